@@ -1,0 +1,182 @@
+"""ctypes mirror of include/acmmp.h (the C-ABI of libacmmp_amd.so).
+
+Struct layouts must match the header byte for byte; tests/test_abi.py checks
+the sizes and that every declared symbol is exported.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "acmmp.h")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libacmmp_amd.so")
+
+MAX_IMAGES = 33
+
+OK = 0
+ERR_ARG = -1
+ERR_STATE = -2
+ERR_HIP = -3
+ERR_IO = -4
+ERR_UNSUPPORTED = -5
+
+
+class Camera(C.Structure):
+    """== struct Camera (src/acmmp_definitions.h:47-55), 100 bytes."""
+
+    _fields_ = [
+        ("K", C.c_float * 9),
+        ("R", C.c_float * 9),
+        ("t", C.c_float * 3),
+        ("height", C.c_int32),
+        ("width", C.c_int32),
+        ("depth_min", C.c_float),
+        ("depth_max", C.c_float),
+    ]
+
+
+class Params(C.Structure):
+    """== struct PatchMatchParams (src/ACMMP.h:32-56) + RNG key."""
+
+    _fields_ = [
+        ("max_iterations", C.c_int32),
+        ("patch_size", C.c_int32),
+        ("num_images", C.c_int32),
+        ("max_image_size", C.c_int32),
+        ("radius_increment", C.c_int32),
+        ("sigma_spatial", C.c_float),
+        ("sigma_color", C.c_float),
+        ("top_k", C.c_int32),
+        ("baseline", C.c_float),
+        ("depth_min", C.c_float),
+        ("depth_max", C.c_float),
+        ("disparity_min", C.c_float),
+        ("disparity_max", C.c_float),
+        ("scaled_cols", C.c_float),
+        ("scaled_rows", C.c_float),
+        ("geom_consistency", C.c_int32),
+        ("planar_prior", C.c_int32),
+        ("multi_geometry", C.c_int32),
+        ("hierarchy", C.c_int32),
+        ("upsample", C.c_int32),
+        ("seeded", C.c_int32),
+        ("seed_lo", C.c_uint32),
+        ("seed_hi", C.c_uint32),
+        ("rng_stream", C.c_uint32),
+        ("reserved", C.c_int32 * 5),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("init_ms", C.c_float),
+        ("sweep_ms", C.c_float),
+        ("sweep_launches", C.c_int32),
+        ("finalize_ms", C.c_float),
+        ("total_ms", C.c_float),
+    ]
+
+
+def default_params() -> Params:
+    """Reference defaults of PatchMatchParams (src/ACMMP.h:32-56), pure Python
+    (no library needed) — must equal acmmp_default_params()."""
+    p = Params()
+    p.max_iterations = 2
+    p.patch_size = 11
+    p.num_images = 5
+    p.max_image_size = 3200
+    p.radius_increment = 2
+    p.sigma_spatial = 5.0
+    p.sigma_color = 3.0
+    p.top_k = 4
+    p.baseline = 0.54
+    p.depth_min = 0.0
+    p.depth_max = 1.0
+    p.disparity_min = 0.0
+    p.disparity_max = 1.0
+    p.seed_lo = 0x5EED
+    p.seed_hi = 0
+    p.rng_stream = 0
+    return p
+
+
+_FP = C.POINTER(C.c_float)
+_U32P = C.POINTER(C.c_uint32)
+_CTX = C.c_void_p
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "acmmp_default_params": (None, [C.POINTER(Params)]),
+    "acmmp_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "acmmp_destroy": (None, [_CTX]),
+    "acmmp_last_error": (C.c_char_p, [_CTX]),
+    "acmmp_set_params": (C.c_int, [_CTX, C.POINTER(Params)]),
+    "acmmp_get_params": (C.c_int, [_CTX, C.POINTER(Params)]),
+    "acmmp_set_geom_consistency_params": (C.c_int, [_CTX, C.c_int]),
+    "acmmp_set_planar_prior_params": (C.c_int, [_CTX]),
+    "acmmp_set_hierarchy_params": (C.c_int, [_CTX]),
+    "acmmp_set_images": (C.c_int, [_CTX, C.c_int, C.POINTER(Camera), C.POINTER(_FP), C.c_int]),
+    "acmmp_set_depth_maps": (C.c_int, [_CTX, C.POINTER(_FP)]),
+    "acmmp_set_depth_maps_device": (C.c_int, [_CTX, C.POINTER(C.c_void_p), C.POINTER(C.c_int32)]),
+    "acmmp_set_images_device": (C.c_int, [_CTX, C.c_int, C.POINTER(Camera), C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_int32), C.c_int]),
+    "acmmp_set_plane_hypotheses_device": (C.c_int, [_CTX, C.c_void_p, C.c_void_p]),
+    "acmmp_export_results": (C.c_int, [_CTX, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "acmmp_set_plane_hypotheses": (C.c_int, [_CTX, _FP, _FP]),
+    "acmmp_set_hierarchy_inputs": (C.c_int, [_CTX, _FP, C.c_int, C.c_int, _FP]),
+    "acmmp_set_seed_prior": (C.c_int, [_CTX, _FP]),
+    "acmmp_set_planar_prior": (C.c_int, [_CTX, _FP, C.c_int, _U32P]),
+    "acmmp_run_patchmatch": (C.c_int, [_CTX]),
+    "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
+    "acmmp_synchronize": (C.c_int, [_CTX]),
+    "acmmp_get_plane_hypotheses": (C.c_int, [_CTX, _FP, C.c_size_t]),
+    "acmmp_get_costs": (C.c_int, [_CTX, _FP, C.c_size_t]),
+    "acmmp_get_selected_views": (C.c_int, [_CTX, _U32P, C.c_size_t]),
+    "acmmp_get_device_results": (C.c_int, [_CTX, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "acmmp_get_reference_size": (C.c_int, [_CTX, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "acmmp_get_camera": (C.c_int, [_CTX, C.c_int, C.POINTER(Camera)]),
+    "acmmp_eval_costs": (C.c_int, [_CTX, _FP, _FP, _FP, _U32P]),
+    "acmmp_eval_geom_costs": (C.c_int, [_CTX, _FP, _FP]),
+    "acmmp_set_timing": (C.c_int, [_CTX, C.c_int]),
+    "acmmp_get_timing": (C.c_int, [_CTX, C.POINTER(Timing)]),
+    "acmmp_device_count": (C.c_int, []),
+    "acmmp_version": (C.c_char_p, []),
+    "acmmp_read_camera": (C.c_int, [C.c_char_p, C.POINTER(Camera)]),
+    "acmmp_read_dmb": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_int32), _FP, C.c_size_t]),
+    "acmmp_write_dmb": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, _FP]),
+}
+
+
+def header_symbols(path: str = HEADER) -> list[str]:
+    """Function names declared in include/acmmp.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(acmmp_[a-z0-9_]+)\s*\(", text)))
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libacmmp_amd.so (built in-tree by __graft_entry__.build()).
+
+    Raises a clear error when the native library is missing: there is no
+    Python or CPU fallback for the product path.
+    """
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libacmmp_amd.so not found at {path}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

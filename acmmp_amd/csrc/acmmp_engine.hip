@@ -1,0 +1,781 @@
+// acmmp_engine.hip — host side of libacmmp_amd.so: the C-ABI declared in
+// include/acmmp.h. Replaces the CUDA host code of the reference's ACMMP class
+// (src/ACMMP.cpp:107-152, :638-831, src/ACMMP.cu:1378-1456) with an engine
+// that owns one HIP stream, keeps all per-view state resident in HBM, enqueues
+// the whole RunPatchMatch without host synchronisation between kernels, and
+// reports failures as status codes instead of exit().
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.h"
+#include "acmmp_internal.h"
+
+using namespace acmmp;
+
+struct acmmp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    acmmp_params prm{};
+    std::string err;
+
+    int n = 0;
+    int W = 0, H = 0, Wh = 0;
+    acmmp_camera cams[ACMMP_MAX_IMAGES]{};
+
+    // device buffers: images / depth maps are either owned (uploaded from the
+    // host, pitched) or borrowed (caller's device pointers, zero copy)
+    std::vector<float *> own_img, own_dep;
+    std::vector<const float *> img, dep;
+    std::vector<int> img_pitch;
+    std::vector<int> dep_pitch, dep_w, dep_h;
+    bool have_depths = false;
+
+    float4 *d_cplane[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [colour][pingpong]
+    float *d_ccost[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    uint32_t *d_csv[2] = {nullptr, nullptr};
+    int cur[2] = {0, 0};
+    float4 *d_rm_plane = nullptr;
+    float *d_rm_cost = nullptr;
+    uint32_t *d_rm_sv = nullptr;
+    float *d_pre_cost = nullptr;
+    float4 *d_prior = nullptr;
+    uint32_t *d_mask = nullptr;
+    float4 *d_scaled = nullptr;
+    size_t scaled_count = 0;
+    float4 *d_seed = nullptr;
+    bool have_prior = false, have_scaled = false, have_seed = false, have_state = false;
+
+    // Per-run constant block. A ring of pinned host / device slots so an
+    // asynchronous run never has its constants overwritten by the next
+    // enqueue: slot k is refilled only after its previous copy completed
+    // (event), and the device copy is stream-ordered behind the kernels that
+    // read it.
+    static constexpr int kSlots = 4;
+    KViews *d_kv_ring[kSlots] = {};
+    KViews *h_kv_ring[kSlots] = {};
+    hipEvent_t kv_ev[kSlots] = {};
+    bool kv_used[kSlots] = {};
+    int kv_slot = 0;
+    KViews *d_kv = nullptr;  // slot of the current enqueue
+    KViews h_kv{};
+
+    bool timing = false;
+    acmmp_timing last_timing{};
+    hipEvent_t ev[8] = {};
+    bool events_made = false;
+};
+
+namespace {
+
+int set_err(acmmp_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, ACMMP_ERR_HIP, "%s failed: %s (%s:%d)", #expr,               \
+                           hipGetErrorString(e_), __FILE__, __LINE__);                       \
+    } while (0)
+
+template <typename T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+template <typename T>
+hipError_t dalloc(T *&p, size_t count) {
+    dfree(p);
+    return hipMalloc((void **)&p, count * sizeof(T) > 0 ? count * sizeof(T) : 4);
+}
+
+int pitch_of(int w) { return (w + 63) / 64 * 64; }
+
+void free_depths(acmmp_ctx *ctx) {
+    for (auto &p : ctx->own_dep) dfree(p);
+    ctx->own_dep.clear();
+    ctx->dep.clear();
+    ctx->dep_pitch.clear();
+    ctx->dep_w.clear();
+    ctx->dep_h.clear();
+    ctx->have_depths = false;
+}
+
+void free_images(acmmp_ctx *ctx) {
+    for (auto &p : ctx->own_img) dfree(p);
+    ctx->own_img.clear();
+    ctx->img.clear();
+    ctx->img_pitch.clear();
+    free_depths(ctx);
+}
+
+void free_state(acmmp_ctx *ctx) {
+    for (int c = 0; c < 2; ++c) {
+        for (int b = 0; b < 2; ++b) {
+            dfree(ctx->d_cplane[c][b]);
+            dfree(ctx->d_ccost[c][b]);
+        }
+        dfree(ctx->d_csv[c]);
+    }
+    dfree(ctx->d_rm_plane);
+    dfree(ctx->d_rm_cost);
+    dfree(ctx->d_rm_sv);
+    dfree(ctx->d_pre_cost);
+    dfree(ctx->d_prior);
+    dfree(ctx->d_mask);
+    dfree(ctx->d_scaled);
+    dfree(ctx->d_seed);
+    ctx->have_prior = ctx->have_scaled = ctx->have_seed = ctx->have_state = false;
+}
+
+// Camera-only part of ComputeHomography (src/ACMMP.cu:264-290), evaluated in
+// the same IEEE order as the reference (this TU builds with -ffp-contract=off).
+ViewRel view_rel(const acmmp_camera &rc, const acmmp_camera &sc) {
+    float ref_C[3], src_C[3];
+    ref_C[0] = -(rc.R[0] * rc.t[0] + rc.R[3] * rc.t[1] + rc.R[6] * rc.t[2]);
+    ref_C[1] = -(rc.R[1] * rc.t[0] + rc.R[4] * rc.t[1] + rc.R[7] * rc.t[2]);
+    ref_C[2] = -(rc.R[2] * rc.t[0] + rc.R[5] * rc.t[1] + rc.R[8] * rc.t[2]);
+    src_C[0] = -(sc.R[0] * sc.t[0] + sc.R[3] * sc.t[1] + sc.R[6] * sc.t[2]);
+    src_C[1] = -(sc.R[1] * sc.t[0] + sc.R[4] * sc.t[1] + sc.R[7] * sc.t[2]);
+    src_C[2] = -(sc.R[2] * sc.t[0] + sc.R[5] * sc.t[1] + sc.R[8] * sc.t[2]);
+    ViewRel r;
+    r.Rr[0] = sc.R[0] * rc.R[0] + sc.R[1] * rc.R[1] + sc.R[2] * rc.R[2];
+    r.Rr[1] = sc.R[0] * rc.R[3] + sc.R[1] * rc.R[4] + sc.R[2] * rc.R[5];
+    r.Rr[2] = sc.R[0] * rc.R[6] + sc.R[1] * rc.R[7] + sc.R[2] * rc.R[8];
+    r.Rr[3] = sc.R[3] * rc.R[0] + sc.R[4] * rc.R[1] + sc.R[5] * rc.R[2];
+    r.Rr[4] = sc.R[3] * rc.R[3] + sc.R[4] * rc.R[4] + sc.R[5] * rc.R[5];
+    r.Rr[5] = sc.R[3] * rc.R[6] + sc.R[4] * rc.R[7] + sc.R[5] * rc.R[8];
+    r.Rr[6] = sc.R[6] * rc.R[0] + sc.R[7] * rc.R[1] + sc.R[8] * rc.R[2];
+    r.Rr[7] = sc.R[6] * rc.R[3] + sc.R[7] * rc.R[4] + sc.R[8] * rc.R[5];
+    r.Rr[8] = sc.R[6] * rc.R[6] + sc.R[7] * rc.R[7] + sc.R[8] * rc.R[8];
+    float Cr[3];
+    Cr[0] = (ref_C[0] - src_C[0]);
+    Cr[1] = (ref_C[1] - src_C[1]);
+    Cr[2] = (ref_C[2] - src_C[2]);
+    r.tr[0] = sc.R[0] * Cr[0] + sc.R[1] * Cr[1] + sc.R[2] * Cr[2];
+    r.tr[1] = sc.R[3] * Cr[0] + sc.R[4] * Cr[1] + sc.R[5] * Cr[2];
+    r.tr[2] = sc.R[6] * Cr[0] + sc.R[7] * Cr[1] + sc.R[8] * Cr[2];
+    return r;
+}
+
+// Rebuilds the device-side constant block from the context.
+int upload_kv(acmmp_ctx *ctx) {
+    KViews &kv = ctx->h_kv;
+    kv.prm = ctx->prm;
+    for (int i = 0; i < ctx->n; ++i) {
+        kv.cam[i] = ctx->cams[i];
+        kv.img[i] = ctx->img[i];
+        kv.ipitch[i] = ctx->img_pitch[i];
+        if (i > 0) kv.rel[i] = view_rel(ctx->cams[0], ctx->cams[i]);
+        if (ctx->have_depths) {
+            kv.dep[i] = ctx->dep[i];
+            kv.dpitch[i] = ctx->dep_pitch[i];
+            kv.dw[i] = ctx->dep_w[i];
+            kv.dh[i] = ctx->dep_h[i];
+        } else {
+            kv.dep[i] = nullptr;
+            kv.dpitch[i] = kv.dw[i] = kv.dh[i] = 0;
+        }
+    }
+    kv.W = ctx->W;
+    kv.H = ctx->H;
+    kv.Wh = ctx->Wh;
+    kv.sweep_rows = checkerboard_rows(ctx->H);
+    kv.nsrc = ctx->n - 1;
+    kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
+    kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
+    kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737
+    kv.pert3_pi = (float)((double)(3 * 0.02f) * M_PI);     // src/ACMMP.cu:649
+    kv.angle_sigma = (float)(M_PI * (double)(5.0f / 180.0f));  // src/ACMMP.cu:715
+    const int k = ctx->kv_slot;
+    ctx->kv_slot = (k + 1) % acmmp_ctx::kSlots;
+    if (!ctx->d_kv_ring[k]) {
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_kv_ring[k], sizeof(KViews)));
+        HIP_TRY(ctx, hipHostMalloc((void **)&ctx->h_kv_ring[k], sizeof(KViews), hipHostMallocDefault));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->kv_ev[k], hipEventDisableTiming));
+    }
+    if (ctx->kv_used[k]) HIP_TRY(ctx, hipEventSynchronize(ctx->kv_ev[k]));
+    std::memcpy(ctx->h_kv_ring[k], &kv, sizeof(KViews));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_kv_ring[k], ctx->h_kv_ring[k], sizeof(KViews), hipMemcpyHostToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->kv_ev[k], ctx->stream));
+    ctx->kv_used[k] = true;
+    ctx->d_kv = ctx->d_kv_ring[k];
+    return ACMMP_OK;
+}
+
+KState make_state(acmmp_ctx *ctx) {
+    KState st{};
+    for (int c = 0; c < 2; ++c) {
+        st.plane[c] = ctx->d_cplane[c][ctx->cur[c]];
+        st.cost[c] = ctx->d_ccost[c][ctx->cur[c]];
+        st.plane_nx[c] = ctx->d_cplane[c][ctx->cur[c] ^ 1];
+        st.cost_nx[c] = ctx->d_ccost[c][ctx->cur[c] ^ 1];
+        st.sv[c] = ctx->d_csv[c];
+    }
+    st.rm_plane = ctx->d_rm_plane;
+    st.rm_cost = ctx->d_rm_cost;
+    st.rm_sv = ctx->d_rm_sv;
+    st.pre_cost = ctx->d_pre_cost;
+    st.prior = ctx->d_prior;
+    st.mask = ctx->d_mask;
+    st.scaled = ctx->d_scaled;
+    st.seed = ctx->d_seed;
+    return st;
+}
+
+int check_ready(acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    if (ctx->n < 2) return set_err(ctx, ACMMP_ERR_STATE, "no images set (acmmp_set_images)");
+    return ACMMP_OK;
+}
+
+int upload_pitched(acmmp_ctx *ctx, float *&dst, int &pitch, const float *src, int w, int h, bool device_src) {
+    pitch = pitch_of(w);
+    HIP_TRY(ctx, dalloc(dst, (size_t)pitch * (size_t)h));
+    HIP_TRY(ctx, hipMemsetAsync(dst, 0, (size_t)pitch * h * sizeof(float), ctx->stream));
+    HIP_TRY(ctx, hipMemcpy2DAsync(dst, (size_t)pitch * sizeof(float), src, (size_t)w * sizeof(float),
+                                  (size_t)w * sizeof(float), (size_t)h,
+                                  device_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+    return ACMMP_OK;
+}
+
+int set_depths_impl(acmmp_ctx *ctx, const float *const *depths, const int32_t *pitches, bool borrow) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!depths) return set_err(ctx, ACMMP_ERR_ARG, "depths is NULL");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // previous run may still read the old maps
+    free_depths(ctx);
+    ctx->own_dep.assign(ctx->n, nullptr);
+    ctx->dep.assign(ctx->n, nullptr);
+    ctx->dep_pitch.assign(ctx->n, 0);
+    ctx->dep_w.assign(ctx->n, 0);
+    ctx->dep_h.assign(ctx->n, 0);
+    for (int i = 0; i < ctx->n; ++i) {
+        if (!depths[i]) return set_err(ctx, ACMMP_ERR_ARG, "depth map %d is NULL", i);
+        const int w = ctx->cams[i].width, h = ctx->cams[i].height;
+        if (borrow) {
+            ctx->dep[i] = depths[i];
+            ctx->dep_pitch[i] = pitches ? pitches[i] : w;
+            if (ctx->dep_pitch[i] < w) return set_err(ctx, ACMMP_ERR_ARG, "depth pitch %d < width %d", ctx->dep_pitch[i], w);
+        } else {
+            rc = upload_pitched(ctx, ctx->own_dep[i], ctx->dep_pitch[i], depths[i], w, h, false);
+            if (rc) return rc;
+            ctx->dep[i] = ctx->own_dep[i];
+        }
+        ctx->dep_w[i] = w;
+        ctx->dep_h[i] = h;
+    }
+    ctx->have_depths = true;
+    if (!borrow) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
+// Shared by acmmp_set_images / acmmp_set_images_device.
+int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, const float *const *images,
+                    const int32_t *pitches, int keep_depth_range, bool borrow) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    if (num_images < 2 || num_images > ACMMP_MAX_IMAGES)
+        return set_err(ctx, ACMMP_ERR_ARG, "num_images=%d outside [2, %d]", num_images, ACMMP_MAX_IMAGES);
+    if (!cams || !images) return set_err(ctx, ACMMP_ERR_ARG, "cams/images NULL");
+    if (ctx->prm.patch_size != 11 || ctx->prm.radius_increment != 2)
+        return set_err(ctx, ACMMP_ERR_UNSUPPORTED,
+                       "patch_size=%d radius_increment=%d: kernels are built for the reference "
+                       "defaults 11/2 (src/ACMMP.h:34,37)",
+                       ctx->prm.patch_size, ctx->prm.radius_increment);
+    for (int i = 0; i < num_images; ++i) {
+        if (!images[i]) return set_err(ctx, ACMMP_ERR_ARG, "image %d is NULL", i);
+        if (cams[i].width <= 0 || cams[i].height <= 0)
+            return set_err(ctx, ACMMP_ERR_ARG, "camera %d has size %dx%d", i, cams[i].width, cams[i].height);
+        if (borrow && pitches && pitches[i] < cams[i].width)
+            return set_err(ctx, ACMMP_ERR_ARG, "image %d pitch %d < width %d", i, pitches[i], cams[i].width);
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    free_images(ctx);
+    const bool resize = (ctx->W != cams[0].width || ctx->H != cams[0].height);
+    ctx->n = num_images;
+    for (int i = 0; i < num_images; ++i) ctx->cams[i] = cams[i];
+    ctx->W = cams[0].width;
+    ctx->H = cams[0].height;
+    ctx->Wh = (ctx->W + 1) / 2;
+    ctx->prm.num_images = num_images;
+    if (!keep_depth_range) {  // InputInitialization (src/ACMMP.cpp:600-606)
+        ctx->prm.depth_min = cams[0].depth_min * 0.6f;
+        ctx->prm.depth_max = cams[0].depth_max * 1.2f;
+        ctx->prm.disparity_min = cams[0].K[0] * ctx->prm.baseline / ctx->prm.depth_max;
+        ctx->prm.disparity_max = cams[0].K[0] * ctx->prm.baseline / ctx->prm.depth_min;
+    }
+    ctx->own_img.assign(num_images, nullptr);
+    ctx->img.assign(num_images, nullptr);
+    ctx->img_pitch.assign(num_images, 0);
+    for (int i = 0; i < num_images; ++i) {
+        if (borrow) {
+            ctx->img[i] = images[i];
+            ctx->img_pitch[i] = pitches ? pitches[i] : cams[i].width;
+        } else {
+            int rc = upload_pitched(ctx, ctx->own_img[i], ctx->img_pitch[i], images[i], cams[i].width,
+                                    cams[i].height, false);
+            if (rc) return rc;
+            ctx->img[i] = ctx->own_img[i];
+        }
+    }
+    if (resize || !ctx->d_rm_plane) {
+        free_state(ctx);
+        const size_t P = (size_t)ctx->W * ctx->H;
+        const size_t Pc = (size_t)ctx->Wh * ctx->H;
+        for (int c = 0; c < 2; ++c) {
+            for (int b = 0; b < 2; ++b) {
+                HIP_TRY(ctx, dalloc(ctx->d_cplane[c][b], Pc));
+                HIP_TRY(ctx, dalloc(ctx->d_ccost[c][b], Pc));
+            }
+            HIP_TRY(ctx, dalloc(ctx->d_csv[c], Pc));
+        }
+        HIP_TRY(ctx, dalloc(ctx->d_rm_plane, P));
+        HIP_TRY(ctx, dalloc(ctx->d_rm_cost, P));
+        HIP_TRY(ctx, dalloc(ctx->d_rm_sv, P));
+        HIP_TRY(ctx, dalloc(ctx->d_pre_cost, P));
+        // zero-filled state (pin: the reference's never-written host fields,
+        // src/ACMMP.cpp:797-804, and uninitialised pre_costs)
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_plane, 0, P * sizeof(float4), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_cost, 0, P * sizeof(float), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_sv, 0, P * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_pre_cost, 0, P * sizeof(float), ctx->stream));
+        for (int c = 0; c < 2; ++c) HIP_TRY(ctx, hipMemsetAsync(ctx->d_csv[c], 0, Pc * sizeof(uint32_t), ctx->stream));
+    }
+    if (!borrow || resize) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.f;
+    return ms;
+}
+
+}  // namespace
+
+extern "C" {
+
+void acmmp_default_params(acmmp_params *p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->max_iterations = 2;
+    p->patch_size = 11;
+    p->num_images = 5;
+    p->max_image_size = 3200;
+    p->radius_increment = 2;
+    p->sigma_spatial = 5.0f;
+    p->sigma_color = 3.0f;
+    p->top_k = 4;
+    p->baseline = 0.54f;
+    p->depth_min = 0.0f;
+    p->depth_max = 1.0f;
+    p->disparity_min = 0.0f;
+    p->disparity_max = 1.0f;
+    p->seed_lo = 0x5EEDu;
+    p->seed_hi = 0u;
+    p->rng_stream = 0u;
+}
+
+int acmmp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *acmmp_version(void) {
+    return "acmmp_amd 0.1 gfx950 (-O3 -ffp-contract=off, IEEE div/sqrt, pinned detmath)";
+}
+
+int acmmp_create(int device, acmmp_ctx **out) {
+    if (!out) return ACMMP_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ACMMP_ERR_HIP;
+    if (device < 0 || device >= ndev) return ACMMP_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    acmmp_ctx *ctx = new acmmp_ctx();
+    ctx->device = device;
+    acmmp_default_params(&ctx->prm);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return ACMMP_ERR_HIP;
+    }
+    *out = ctx;
+    return ACMMP_OK;
+}
+
+void acmmp_destroy(acmmp_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_images(ctx);
+    free_state(ctx);
+    for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
+        dfree(ctx->d_kv_ring[k]);
+        if (ctx->h_kv_ring[k]) (void)hipHostFree(ctx->h_kv_ring[k]);
+        if (ctx->kv_ev[k]) (void)hipEventDestroy(ctx->kv_ev[k]);
+    }
+    if (ctx->events_made)
+        for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *acmmp_last_error(const acmmp_ctx *ctx) {
+    if (!ctx) return "null context";
+    return ctx->err.c_str();
+}
+
+int acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *p) {
+    if (!ctx || !p) return ACMMP_ERR_ARG;
+    ctx->prm = *p;
+    if (ctx->n >= 2) ctx->prm.num_images = ctx->n;
+    return ACMMP_OK;
+}
+
+int acmmp_get_params(const acmmp_ctx *ctx, acmmp_params *p) {
+    if (!ctx || !p) return ACMMP_ERR_ARG;
+    *p = ctx->prm;
+    return ACMMP_OK;
+}
+
+int acmmp_set_geom_consistency_params(acmmp_ctx *ctx, int multi_geometry) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    ctx->prm.geom_consistency = 1;
+    ctx->prm.max_iterations = 2;  // src/ACMMP.cpp:450
+    if (multi_geometry) ctx->prm.multi_geometry = 1;
+    return ACMMP_OK;
+}
+
+int acmmp_set_planar_prior_params(acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    ctx->prm.planar_prior = 1;
+    return ACMMP_OK;
+}
+
+int acmmp_set_hierarchy_params(acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    ctx->prm.hierarchy = 1;
+    return ACMMP_OK;
+}
+
+int acmmp_set_images(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, const float *const *images,
+                     int keep_depth_range) {
+    return set_images_impl(ctx, num_images, cams, images, nullptr, keep_depth_range, false);
+}
+
+int acmmp_set_images_device(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
+                            const float *const *d_images, const int32_t *pitches, int keep_depth_range) {
+    return set_images_impl(ctx, num_images, cams, d_images, pitches, keep_depth_range, true);
+}
+
+int acmmp_set_depth_maps(acmmp_ctx *ctx, const float *const *depths) {
+    return set_depths_impl(ctx, depths, nullptr, false);
+}
+
+int acmmp_set_depth_maps_device(acmmp_ctx *ctx, const float *const *d_depths, const int32_t *pitches) {
+    return set_depths_impl(ctx, d_depths, pitches, true);
+}
+
+int acmmp_set_plane_hypotheses(acmmp_ctx *ctx, const float *planes4, const float *costs) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!planes4 || !costs) return set_err(ctx, ACMMP_ERR_ARG, "planes/costs NULL");
+    const size_t P = (size_t)ctx->W * ctx->H;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, planes4, P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_cost, costs, P * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->have_state = true;
+    return ACMMP_OK;
+}
+
+int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, const float *d_costs) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!d_planes4 || !d_costs) return set_err(ctx, ACMMP_ERR_ARG, "planes/costs NULL");
+    const size_t P = (size_t)ctx->W * ctx->H;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, d_planes4, P * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_cost, d_costs, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->have_state = true;
+    return ACMMP_OK;
+}
+
+int acmmp_export_results(acmmp_ctx *ctx, float *d_planes4, float *d_costs, float *d_depth) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    if (d_planes4)
+        HIP_TRY(ctx, hipMemcpyAsync(d_planes4, ctx->d_rm_plane, P * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_costs)
+        HIP_TRY(ctx, hipMemcpyAsync(d_costs, ctx->d_rm_cost, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_depth)  // the .w channel: strided 2-D copy, 4 B out of every 16 B
+        HIP_TRY(ctx, hipMemcpy2DAsync(d_depth, sizeof(float), (const char *)ctx->d_rm_plane + 3 * sizeof(float),
+                                      sizeof(float4), sizeof(float), P, hipMemcpyDeviceToDevice, ctx->stream));
+    return ACMMP_OK;
+}
+
+int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w, int scaled_h,
+                               const float *upsampled_depth) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!scaled_planes4 || !upsampled_depth || scaled_w <= 0 || scaled_h <= 0)
+        return set_err(ctx, ACMMP_ERR_ARG, "bad hierarchy inputs");
+    const size_t S = (size_t)scaled_w * scaled_h;
+    HIP_TRY(ctx, dalloc(ctx->d_scaled, S));
+    ctx->scaled_count = S;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_scaled, scaled_planes4, S * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    // plane_hypotheses_host[center].w = ref_depth; x, y, z never written (pinned 0)
+    const size_t P = (size_t)ctx->W * ctx->H;
+    std::vector<float> tmp(P * 4, 0.0f);
+    for (size_t i = 0; i < P; ++i) tmp[i * 4 + 3] = upsampled_depth[i];
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, tmp.data(), P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    // `if (width != images[0].rows || height != images[0].cols)` (src/ACMMP.cpp:766), swap included
+    if (scaled_w != ctx->H || scaled_h != ctx->W) {
+        ctx->prm.upsample = 1;
+        ctx->prm.scaled_cols = (float)scaled_w;
+        ctx->prm.scaled_rows = (float)scaled_h;
+    } else {
+        ctx->prm.upsample = 0;
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->have_scaled = true;
+    return ACMMP_OK;
+}
+
+int acmmp_set_seed_prior(acmmp_ctx *ctx, const float *planes4) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!planes4) return set_err(ctx, ACMMP_ERR_ARG, "planes NULL");
+    const size_t P = (size_t)ctx->W * ctx->H;
+    HIP_TRY(ctx, dalloc(ctx->d_seed, P));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_seed, planes4, P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->prm.seeded = 1;
+    ctx->have_seed = true;
+    return ACMMP_OK;
+}
+
+int acmmp_set_planar_prior(acmmp_ctx *ctx, const float *plane_params4, int num_planes, const uint32_t *mask) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!mask || num_planes < 0 || (num_planes > 0 && !plane_params4))
+        return set_err(ctx, ACMMP_ERR_ARG, "bad planar prior inputs");
+    const size_t P = (size_t)ctx->W * ctx->H;
+    // CudaPlanarPriorInitialization (src/ACMMP.cpp:811-831): expand the label
+    // mask into a per-pixel plane array (unlabelled pixels: zero, pinned).
+    std::vector<float> planes(P * 4, 0.0f);
+    for (size_t i = 0; i < P; ++i) {
+        const uint32_t m = mask[i];
+        if (m > 0) {
+            if ((int)m > num_planes)
+                return set_err(ctx, ACMMP_ERR_ARG, "mask label %u exceeds %d planes", m, num_planes);
+            std::memcpy(&planes[i * 4], plane_params4 + (size_t)(m - 1) * 4, 4 * sizeof(float));
+        }
+    }
+    HIP_TRY(ctx, dalloc(ctx->d_prior, P));
+    HIP_TRY(ctx, dalloc(ctx->d_mask, P));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_prior, planes.data(), P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_mask, mask, P * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->have_prior = true;
+    return ACMMP_OK;
+}
+
+int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const acmmp_params &p = ctx->prm;
+    if (p.geom_consistency && !ctx->have_depths)
+        return set_err(ctx, ACMMP_ERR_STATE, "geom_consistency needs depth maps (acmmp_set_depth_maps)");
+    if (p.planar_prior && !ctx->have_prior)
+        return set_err(ctx, ACMMP_ERR_STATE, "planar_prior needs acmmp_set_planar_prior");
+    if (p.hierarchy && !ctx->have_scaled)
+        return set_err(ctx, ACMMP_ERR_STATE, "hierarchy needs acmmp_set_hierarchy_inputs");
+    if (p.seeded && !ctx->have_seed) return set_err(ctx, ACMMP_ERR_STATE, "seeded needs acmmp_set_seed_prior");
+    if (p.patch_size != 11 || p.radius_increment != 2)
+        return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "only patch_size 11 / radius_increment 2 are built");
+    if (p.max_iterations < 0) return set_err(ctx, ACMMP_ERR_ARG, "max_iterations < 0");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    rc = upload_kv(ctx);
+    if (rc) return rc;
+    if (ctx->timing && !ctx->events_made) {
+        for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
+        ctx->events_made = true;
+    }
+    hipStream_t s = ctx->stream;
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
+    ctx->cur[0] = ctx->cur[1] = 0;
+    HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, make_state(ctx), s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
+    for (int it = 0; it < p.max_iterations; ++it) {
+        for (int colour = 0; colour < 2; ++colour) {  // BlackPixelUpdate, RedPixelUpdate
+            HIP_TRY(ctx, launch_sweep(ctx->d_kv, ctx->h_kv, make_state(ctx), colour, it, s));
+            ctx->cur[colour] ^= 1;
+        }
+    }
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
+    HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, make_state(ctx), s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, make_state(ctx), 0, s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, make_state(ctx), 1, s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
+    ctx->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
+    ctx->have_state = true;
+    return ACMMP_OK;
+}
+
+int acmmp_synchronize(acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->timing && ctx->events_made) {
+        acmmp_timing &t = ctx->last_timing;
+        t.init_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+        t.sweep_ms = elapsed(ctx->ev[1], ctx->ev[2]);
+        t.sweep_launches = 2 * ctx->prm.max_iterations;
+        t.finalize_ms = elapsed(ctx->ev[2], ctx->ev[3]);
+        t.total_ms = elapsed(ctx->ev[0], ctx->ev[3]);
+    }
+    return ACMMP_OK;
+}
+
+int acmmp_run_patchmatch(acmmp_ctx *ctx) {
+    int rc = acmmp_run_patchmatch_async(ctx);
+    if (rc) return rc;
+    return acmmp_synchronize(ctx);
+}
+
+int acmmp_get_plane_hypotheses(acmmp_ctx *ctx, float *planes4, size_t n) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    if (!planes4 || n < P) return set_err(ctx, ACMMP_ERR_ARG, "output capacity %zu < %zu", n, P);
+    HIP_TRY(ctx, hipMemcpyAsync(planes4, ctx->d_rm_plane, P * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
+int acmmp_get_costs(acmmp_ctx *ctx, float *costs, size_t n) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    if (!costs || n < P) return set_err(ctx, ACMMP_ERR_ARG, "output capacity %zu < %zu", n, P);
+    HIP_TRY(ctx, hipMemcpyAsync(costs, ctx->d_rm_cost, P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
+int acmmp_get_selected_views(acmmp_ctx *ctx, uint32_t *views, size_t n) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    if (!views || n < P) return set_err(ctx, ACMMP_ERR_ARG, "output capacity %zu < %zu", n, P);
+    HIP_TRY(ctx, hipMemcpyAsync(views, ctx->d_rm_sv, P * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
+int acmmp_get_device_results(acmmp_ctx *ctx, const float **d_planes4, const float **d_costs) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (d_planes4) *d_planes4 = (const float *)ctx->d_rm_plane;
+    if (d_costs) *d_costs = ctx->d_rm_cost;
+    return ACMMP_OK;
+}
+
+int acmmp_get_reference_size(const acmmp_ctx *ctx, int *width, int *height) {
+    if (!ctx || !width || !height) return ACMMP_ERR_ARG;
+    *width = ctx->W;
+    *height = ctx->H;
+    return ACMMP_OK;
+}
+
+int acmmp_get_camera(const acmmp_ctx *ctx, int index, acmmp_camera *cam) {
+    if (!ctx || !cam || index < 0 || index >= ctx->n) return ACMMP_ERR_ARG;
+    *cam = ctx->cams[index];
+    return ACMMP_OK;
+}
+
+int acmmp_eval_costs(acmmp_ctx *ctx, const float *planes4, float *out_costs, float *out_init_cost,
+                     uint32_t *out_init_views) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!planes4) return set_err(ctx, ACMMP_ERR_ARG, "planes NULL");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    rc = upload_kv(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    const int ns = ctx->n - 1;
+    float4 *d_pl = nullptr;
+    float *d_out = nullptr, *d_init = nullptr;
+    uint32_t *d_views = nullptr;
+    HIP_TRY(ctx, dalloc(d_pl, P));
+    if (out_costs) HIP_TRY(ctx, dalloc(d_out, P * ns));
+    if (out_init_cost) HIP_TRY(ctx, dalloc(d_init, P));
+    if (out_init_views) HIP_TRY(ctx, dalloc(d_views, P));
+    HIP_TRY(ctx, hipMemcpyAsync(d_pl, planes4, P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_eval_costs(ctx->d_kv, ctx->h_kv, d_pl, d_out, d_init, d_views, ctx->stream));
+    if (out_costs)
+        HIP_TRY(ctx, hipMemcpyAsync(out_costs, d_out, P * ns * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (out_init_cost)
+        HIP_TRY(ctx, hipMemcpyAsync(out_init_cost, d_init, P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (out_init_views)
+        HIP_TRY(ctx, hipMemcpyAsync(out_init_views, d_views, P * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    dfree(d_pl);
+    dfree(d_out);
+    dfree(d_init);
+    dfree(d_views);
+    return ACMMP_OK;
+}
+
+int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!planes4 || !out) return set_err(ctx, ACMMP_ERR_ARG, "NULL argument");
+    if (!ctx->have_depths) return set_err(ctx, ACMMP_ERR_STATE, "no depth maps");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    rc = upload_kv(ctx);
+    if (rc) return rc;
+    const size_t P = (size_t)ctx->W * ctx->H;
+    const int ns = ctx->n - 1;
+    float4 *d_pl = nullptr;
+    float *d_out = nullptr;
+    HIP_TRY(ctx, dalloc(d_pl, P));
+    HIP_TRY(ctx, dalloc(d_out, P * ns));
+    HIP_TRY(ctx, hipMemcpyAsync(d_pl, planes4, P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_eval_geom(ctx->d_kv, ctx->h_kv, d_pl, d_out, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(out, d_out, P * ns * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    dfree(d_pl);
+    dfree(d_out);
+    return ACMMP_OK;
+}
+
+int acmmp_set_timing(acmmp_ctx *ctx, int enable) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    ctx->timing = enable != 0;
+    return ACMMP_OK;
+}
+
+int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t) {
+    if (!ctx || !t) return ACMMP_ERR_ARG;
+    *t = ctx->last_timing;
+    return ACMMP_OK;
+}
+
+}  // extern "C"

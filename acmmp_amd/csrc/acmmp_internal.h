@@ -1,0 +1,85 @@
+// acmmp_internal.h — device-side data layout shared by the kernels
+// (acmmp_kernels.hip) and the host engine (acmmp_engine.hip).
+//
+// HBM layout (per engine = per reference view being processed):
+//   * source images: one pitched fp32 buffer per view (pitch = width rounded
+//     up to 64 floats = 256 B, so every row starts on a 256-B boundary).
+//   * PatchMatch state during the sweeps is stored COLOUR-SPLIT: pixel (x, y)
+//     has colour c = (x + y) & 1 and lives at index y * Wh + (x >> 1) of the
+//     colour-c plane, Wh = ceil(W / 2). A half-sweep of colour c reads both
+//     colour planes and writes only colour c, so a wave's 64 lanes touch 64
+//     consecutive elements of every array it streams (coalesced), and
+//     same-colour snapshot reads (reference race) are
+//     served by ping-pong buffers of the written colour with no copy.
+//   * between runs the state is row-major (`rm_*`): exactly the reference's
+//     plane_hypotheses_cuda / costs_cuda / selected_views_cuda, which the
+//     init kernel reads and the finalize + filter kernels write.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/acmmp.h"
+
+namespace acmmp {
+
+// Per-view geometry derived from the two cameras, identical expressions to
+// ComputeHomography's camera-only part (src/ACMMP.cu:264-290).
+struct ViewRel {
+    float Rr[9];   // R_relative
+    float tr[3];   // t_relative
+};
+
+struct KViews {
+    acmmp_params prm;
+    acmmp_camera cam[ACMMP_MAX_IMAGES];
+    ViewRel rel[ACMMP_MAX_IMAGES];            // rel[v] for source v (1-based), rel[0] unused
+    const float *img[ACMMP_MAX_IMAGES];       // pitched images
+    int ipitch[ACMMP_MAX_IMAGES];             // in floats
+    const float *dep[ACMMP_MAX_IMAGES];       // pitched depth maps (geom consistency)
+    int dpitch[ACMMP_MAX_IMAGES];
+    int dw[ACMMP_MAX_IMAGES];
+    int dh[ACMMP_MAX_IMAGES];
+    int W, H, Wh, sweep_rows, nsrc;
+    float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
+    float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
+};
+
+struct KState {
+    float4 *plane[2];       // colour-split current (read) planes, [colour]
+    float *cost[2];
+    float4 *plane_nx[2];    // colour-split next (written) planes
+    float *cost_nx[2];
+    uint32_t *sv[2];        // colour-split selected views (in place)
+    float4 *rm_plane;       // row-major state between runs
+    float *rm_cost;
+    uint32_t *rm_sv;
+    float *pre_cost;        // hierarchy (row-major)
+    const float4 *prior;    // planar prior planes (row-major)
+    const uint32_t *mask;   // planar prior triangle labels
+    const float4 *scaled;   // hierarchy low-res planes (scaled_rows x scaled_cols)
+    const float4 *seed;     // seeded priors
+};
+
+// Kernel launchers (acmmp_kernels.hip). All enqueue on `stream`.
+hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream);
+hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                        int iter, hipStream_t stream);
+hipError_t launch_finalize(const KViews *d_kv, const KViews &h_kv, const KState &st,
+                           hipStream_t stream);
+hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                         hipStream_t stream);
+hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float4 *planes,
+                             float *out_costs, float *out_init, uint32_t *out_views,
+                             hipStream_t stream);
+hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4 *planes,
+                            float *out, hipStream_t stream);
+
+// Number of checkerboard rows the reference grid reaches (src/ACMMP.cu:1399).
+inline int checkerboard_rows(int H) {
+    int gy = ((H / 2) + 16 - 1) / 16;
+    int rows = gy * 32;
+    return rows < H ? rows : H;
+}
+
+}  // namespace acmmp

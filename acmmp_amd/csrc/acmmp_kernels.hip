@@ -1,0 +1,1139 @@
+// acmmp_kernels.hip — MI355X (gfx950, CDNA4) kernels for ACMMP::RunPatchMatch.
+//
+// Reference semantics: rlav440/ACMMP src/ACMMP.cu:17-1352 (device code) with the
+// pinned semantics of SURVEY.md Appendix A and the arithmetic pins P1-P4 listed
+// in oracle/acmmp_oracle.c / DESIGN.md §4. The CPU oracle restates the
+// reference literally; this file is the GPU design:
+//
+//  * one lane per pixel, 64-lane waves laid along a row of ONE checkerboard
+//    colour (colour-split layout, acmmp_internal.h) so every state access of
+//    a wave is a contiguous 256-B..1-KiB segment;
+//  * the reference patch of a pixel (36 bilateral weights w and w*ref, the
+//    normalised ref mean/variance) is invariant across the 14*(N-1)
+//    ComputeBilateralNCC calls of a pixel-iteration: it is computed once per
+//    pixel-iteration into VGPRs (exact: same operations, same order);
+//  * NCC calls for views whose sampled view weight is 0 are skipped: the
+//    reference multiplies their (finite, >= 0) cost by 0 and adds +0, so the
+//    result is bit-identical (refinement at :751 skips them explicitly);
+//  * stateless Philox RNG (no 48-B curandState traffic per pixel);
+//  * all per-launch constants (cameras, homography camera terms, image
+//    pointers) sit in one device struct read through scalar loads.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "../../include/acmmp_detmath.h"
+#include "acmmp_internal.h"
+
+namespace acmmp {
+
+#define DEV static __device__ __forceinline__
+
+// Patch geometry fixed by the reference defaults (patch_size 11, increment 2:
+// offsets {-5,-3,-1,1,3,5}^2, src/ACMMP.h:34,37). The engine rejects others.
+constexpr int kTaps = 6;
+constexpr int kSamples = kTaps * kTaps;
+
+// ----------------------------------------------------------------- textures
+DEV float texel(const float *img, int pitch, int W, int H, int x, int y) {
+    x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
+    y = y < 0 ? 0 : (y > H - 1 ? H - 1 : y);
+    return img[y * pitch + x];
+}
+
+// pin P2 (tex2D linear, clamp; src/ACMMP.cu:394)
+DEV float bilinear(const float *img, int pitch, int W, int H, float u, float v) {
+    float xs = (u + 0.5f) - 0.5f;
+    float ys = (v + 0.5f) - 0.5f;
+    const float fw = (float)W, fh = (float)H;
+    xs = (xs > -1.0f) ? xs : -1.0f;
+    xs = (xs < fw) ? xs : fw;
+    ys = (ys > -1.0f) ? ys : -1.0f;
+    ys = (ys < fh) ? ys : fh;
+    const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
+    const float ax = xs - fx0, ay = ys - fy0;
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const int xa = x0 < 0 ? 0 : x0;
+    const int xb = (x0 + 1) > (W - 1) ? (W - 1) : (x0 + 1);
+    const int ya = y0 < 0 ? 0 : y0;
+    const int yb = (y0 + 1) > (H - 1) ? (H - 1) : (y0 + 1);
+    const int xa2 = xa > W - 1 ? W - 1 : xa;
+    const int ya2 = ya > H - 1 ? H - 1 : ya;
+    const int xb2 = xb < 0 ? 0 : xb;
+    const int yb2 = yb < 0 ? 0 : yb;
+    const float *r0 = img + ya2 * pitch;
+    const float *r1 = img + yb2 * pitch;
+    const float t00 = r0[xa2], t10 = r0[xb2];
+    const float t01 = r1[xa2], t11 = r1[xb2];
+    const float top = dm_fma(ax, t10 - t00, t00);
+    const float bot = dm_fma(ax, t11 - t01, t01);
+    return dm_fma(ay, bot - top, top);
+}
+
+// tex2D(depth, (int)x + 0.5, (int)y + 0.5) (src/ACMMP.cu:528)
+DEV float tex_trunc(const float *img, int pitch, int W, int H, float u, float v) {
+    const float fw = (float)W, fh = (float)H;
+    u = (u > -1.0f) ? u : -1.0f;
+    u = (u < fw) ? u : fw;
+    v = (v > -1.0f) ? v : -1.0f;
+    v = (v < fh) ? v : fh;
+    return texel(img, pitch, W, H, (int)u, (int)v);
+}
+
+// ------------------------------------------------------------ geometry
+// Get3DPoint (src/ACMMP.cu:123-128)
+DEV void get3d(const acmmp_camera &c, int px, int py, float depth, float *X) {
+    X[0] = depth * ((float)px - c.K[2]) / c.K[0];
+    X[1] = depth * ((float)py - c.K[5]) / c.K[4];
+    X[2] = depth;
+}
+
+// GetViewDirection (src/ACMMP.cu:130-142)
+DEV float4 view_direction(const acmmp_camera &c, int px, int py, float depth) {
+    float X[3];
+    get3d(c, px, py, depth, X);
+    const float norm = dm_sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+    return make_float4(X[0] / norm, X[1] / norm, X[2] / norm, 0.0f);
+}
+
+// GetDistance2Origin (src/ACMMP.cu:144-149)
+DEV float distance_to_origin(const acmmp_camera &c, int px, int py, float depth, float4 n) {
+    float X[3];
+    get3d(c, px, py, depth, X);
+    return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
+}
+
+// ComputeDepthfromPlaneHypothesis (src/ACMMP.cu:163-168)
+DEV float plane_depth(const acmmp_camera &c, float4 h, int px, int py) {
+    return -h.w * c.K[0] /
+           (((float)px - c.K[2]) * h.x + (c.K[0] / c.K[4]) * ((float)py - c.K[5]) * h.y + c.K[0] * h.z);
+}
+
+// NormalizeVec3 (src/ACMMP.cu:98-105), rsqrt pinned to 1/sqrt
+DEV void normalize3(float4 &v) {
+    const float n2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float inv = dm_rsqrt(n2);
+    v.x *= inv;
+    v.y *= inv;
+    v.z *= inv;
+}
+
+DEV float dot3(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// TransformNormal cam->world (src/ACMMP.cu:333-341)
+DEV float4 to_world(const acmmp_camera &c, float4 h) {
+    return make_float4(c.R[0] * h.x + c.R[3] * h.y + c.R[6] * h.z,
+                       c.R[1] * h.x + c.R[4] * h.y + c.R[7] * h.z,
+                       c.R[2] * h.x + c.R[5] * h.y + c.R[8] * h.z, h.w);
+}
+
+// TransformNormal2RefCam world->cam (src/ACMMP.cu:343-351)
+DEV float4 to_cam(const acmmp_camera &c, float4 h) {
+    return make_float4(c.R[0] * h.x + c.R[1] * h.y + c.R[2] * h.z,
+                       c.R[3] * h.x + c.R[4] * h.y + c.R[5] * h.z,
+                       c.R[6] * h.x + c.R[7] * h.y + c.R[8] * h.z, h.w);
+}
+
+// GenerateRandomNormal (src/ACMMP.cu:170-196)
+DEV float4 random_normal(const acmmp_camera &c, int px, int py, dm_rng &rs, float depth) {
+    float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
+    int guard = 0;
+    while (s >= 1.0f && guard < 1000) {
+        q1 = 2.0f * dm_rng_uniform(&rs) - 1.0f;
+        q2 = 2.0f * dm_rng_uniform(&rs) - 1.0f;
+        s = q1 * q1 + q2 * q2;
+        ++guard;
+    }
+    const float sq = dm_sqrt(1.0f - s);
+    float4 n = make_float4(2.0f * q1 * sq, 2.0f * q2 * sq, 1.0f - 2.0f * s, 0.0f);
+    const float4 vd = view_direction(c, px, py, depth);
+    if (n.x * vd.x + n.y * vd.y + n.z * vd.z > 0.0f) {
+        n.x = -n.x;
+        n.y = -n.y;
+        n.z = -n.z;
+    }
+    normalize3(n);
+    return n;
+}
+
+// GeneratePerturbedNormal (src/ACMMP.cu:198-233)
+DEV float4 perturbed_normal(const acmmp_camera &c, int px, int py, float4 normal, dm_rng &rs,
+                            float perturbation) {
+    const float4 vd = view_direction(c, px, py, 1.0f);
+    const float a1 = (dm_rng_uniform(&rs) - 0.5f) * perturbation;
+    const float a2 = (dm_rng_uniform(&rs) - 0.5f) * perturbation;
+    const float a3 = (dm_rng_uniform(&rs) - 0.5f) * perturbation;
+    const float s1 = dm_sinf(a1), s2 = dm_sinf(a2), s3 = dm_sinf(a3);
+    const float c1 = dm_cosf(a1), c2 = dm_cosf(a2), c3 = dm_cosf(a3);
+    float R[9];
+    R[0] = c2 * c3;
+    R[1] = c3 * s1 * s2 - c1 * s3;
+    R[2] = s1 * s3 + c1 * c3 * s2;
+    R[3] = c2 * s3;
+    R[4] = c1 * c3 + s1 * s2 * s3;
+    R[5] = c1 * s2 * s3 - c3 * s1;
+    R[6] = -s2;
+    R[7] = c2 * s1;
+    R[8] = c1 * c2;
+    float4 np = make_float4(R[0] * normal.x + R[1] * normal.y + R[2] * normal.z,
+                            R[3] * normal.x + R[4] * normal.y + R[5] * normal.z,
+                            R[6] * normal.x + R[7] * normal.y + R[8] * normal.z, normal.w);
+    if (dot3(np, vd) >= 0.0f) np = normal;
+    normalize3(np);
+    return np;
+}
+
+// ------------------------------------------------------ homography + NCC
+// ComputeHomography (src/ACMMP.cu:262-322) with the camera-only terms
+// precomputed per view (ViewRel) and pin P4.
+DEV void homography(const KViews &kv, int v, float4 h, float *H) {
+    const ViewRel &r = kv.rel[v];
+    const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
+    const float inv_w = 1.0f / h.w;
+    float G[9];
+    G[0] = r.Rr[0] - (r.tr[0] * h.x) * inv_w;
+    G[1] = r.Rr[1] - (r.tr[0] * h.y) * inv_w;
+    G[2] = r.Rr[2] - (r.tr[0] * h.z) * inv_w;
+    G[3] = r.Rr[3] - (r.tr[1] * h.x) * inv_w;
+    G[4] = r.Rr[4] - (r.tr[1] * h.y) * inv_w;
+    G[5] = r.Rr[5] - (r.tr[1] * h.z) * inv_w;
+    G[6] = r.Rr[6] - (r.tr[2] * h.x) * inv_w;
+    G[7] = r.Rr[7] - (r.tr[2] * h.y) * inv_w;
+    G[8] = r.Rr[8] - (r.tr[2] * h.z) * inv_w;
+    const float ik0 = kv.inv_k0, ik4 = kv.inv_k4;
+    float t[9];
+    t[0] = G[0] * ik0;
+    t[1] = G[1] * ik4;
+    t[2] = ((-G[0] * rc.K[2]) * ik0 - (G[1] * rc.K[5]) * ik4) + G[2];
+    t[3] = G[3] * ik0;
+    t[4] = G[4] * ik4;
+    t[5] = ((-G[3] * rc.K[2]) * ik0 - (G[4] * rc.K[5]) * ik4) + G[5];
+    t[6] = G[6] * ik0;
+    t[7] = G[7] * ik4;
+    t[8] = ((-G[6] * rc.K[2]) * ik0 - (G[7] * rc.K[5]) * ik4) + G[8];
+    H[0] = sc.K[0] * t[0] + sc.K[2] * t[6];
+    H[1] = sc.K[0] * t[1] + sc.K[2] * t[7];
+    H[2] = sc.K[0] * t[2] + sc.K[2] * t[8];
+    H[3] = sc.K[4] * t[3] + sc.K[5] * t[6];
+    H[4] = sc.K[4] * t[4] + sc.K[5] * t[7];
+    H[5] = sc.K[4] * t[5] + sc.K[5] * t[8];
+    H[6] = sc.K[8] * t[6];
+    H[7] = sc.K[8] * t[7];
+    H[8] = sc.K[8] * t[8];
+}
+
+// ComputeCorrespondingPoint (src/ACMMP.cu:324-331), pin P1
+DEV float2 project(const float *H, float x, float y) {
+    const float px = dm_fma(H[0], x, dm_fma(H[1], y, H[2]));
+    const float py = dm_fma(H[3], x, dm_fma(H[4], y, H[5]));
+    const float pz = dm_fma(H[6], x, dm_fma(H[7], y, H[8]));
+    const float inv = 1.0f / pz;
+    return make_float2(px * inv, py * inv);
+}
+
+// Invariant reference-side part of ComputeBilateralNCC (src/ACMMP.cu:372-421):
+// everything that does not depend on the source view or the plane.
+struct RefPatch {
+    float w[kSamples];
+    float wr[kSamples];
+    float mean;      // sum_ref * inv_bilateral_weight_sum
+    float var;       // var_ref
+    float inv_wsum;  // inv_bilateral_weight_sum
+};
+
+// ComputeBilateralWeight (src/ACMMP.cu:353-358)
+DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
+    const float spatial = dm_sqrt(xd * xd + yd * yd);
+    const float color = dm_fabs(pix - cpix);
+    return dm_expf(-spatial / (2.0f * ss * ss) - color / (2.0f * sc * sc));
+}
+
+DEV void ref_patch(const KViews &kv, int px, int py, RefPatch &rp) {
+    const float *img = kv.img[0];
+    const int pitch = kv.ipitch[0], W = kv.W, H = kv.H;
+    const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
+    const float center = texel(img, pitch, W, H, px, py);
+    float sum_ref = 0.0f, sum_rr = 0.0f, bw = 0.0f;
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        const int i = -5 + 2 * ii;
+        float r_ref = 0.0f, r_rr = 0.0f, r_w = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < kTaps; ++jj) {
+            const int j = -5 + 2 * jj;
+            const float r = texel(img, pitch, W, H, px + i, py + j);
+            const float w = bilateral_weight((float)i, (float)j, r, center, ss, sc);
+            const float wr = w * r;
+            r_ref += wr;
+            r_rr = dm_fma(wr, r, r_rr);
+            r_w += w;
+            rp.w[ii * kTaps + jj] = w;
+            rp.wr[ii * kTaps + jj] = wr;
+        }
+        sum_ref += r_ref;
+        sum_rr += r_rr;
+        bw += r_w;
+    }
+    const float inv = 1.0f / bw;
+    sum_ref *= inv;
+    sum_rr *= inv;
+    rp.mean = sum_ref;
+    rp.var = sum_rr - sum_ref * sum_ref;
+    rp.inv_wsum = inv;
+}
+
+// ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based).
+DEV float bilateral_ncc(const KViews &kv, const RefPatch &rp, int v, int px, int py, float4 h) {
+    const float cost_max = 2.0f;
+    const float kMinVar = 1e-5f;
+    // var_ref is invariant: when it is below kMinVar (or the centre maps
+    // outside the source) every call returns cost_max.
+    if (rp.var < kMinVar) return cost_max;
+    const acmmp_camera &sc = kv.cam[v];
+    const int sW = sc.width, sH = sc.height;
+    float H[9];
+    homography(kv, v, h, H);
+    const float2 pt = project(H, (float)px, (float)py);
+    if (pt.x >= (float)sW || pt.x < 0.0f || pt.y >= (float)sH || pt.y < 0.0f) return cost_max;
+    const float *img = kv.img[v];
+    const int pitch = kv.ipitch[v];
+    float sum_src = 0.0f, sum_ss = 0.0f, sum_rs = 0.0f;
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        const float x = (float)(px - 5 + 2 * ii);
+        float r_s = 0.0f, r_ss = 0.0f, r_rs = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < kTaps; ++jj) {
+            const float y = (float)(py - 5 + 2 * jj);
+            const float2 q = project(H, x, y);
+            const float s = bilinear(img, pitch, sW, sH, q.x, q.y);
+            const float ws = rp.w[ii * kTaps + jj] * s;
+            r_s += ws;
+            r_ss = dm_fma(ws, s, r_ss);
+            r_rs = dm_fma(rp.wr[ii * kTaps + jj], s, r_rs);
+        }
+        sum_src += r_s;
+        sum_ss += r_ss;
+        sum_rs += r_rs;
+    }
+    sum_src *= rp.inv_wsum;
+    sum_ss *= rp.inv_wsum;
+    sum_rs *= rp.inv_wsum;
+    const float var_src = sum_ss - sum_src * sum_src;
+    if (var_src < kMinVar) return cost_max;
+    const float covar = sum_rs - rp.mean * sum_src;
+    const float var_rs = dm_sqrt(rp.var * var_src);
+    float c = 1.0f - covar / var_rs;
+    c = (c < cost_max) ? c : cost_max;
+    c = (c > 0.0f) ? c : 0.0f;
+    return c;
+}
+
+// ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
+template <int NS>
+DEV float initial_cost(const KViews &kv, const RefPatch &rp, int px, int py, float4 h, uint32_t &sel) {
+    const int nsrc = kv.nsrc;
+    float cv[NS];
+    float cs[NS];
+    int num_valid = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        const float c = bilateral_ncc(kv, rp, i + 1, px, py, h);
+        cv[i] = c;
+        cs[i] = c;
+        if (c < 2.0f) num_valid++;
+    }
+    // sort_small (src/ACMMP.cu:24-33)
+    for (int i = 1; i < nsrc; i++) {
+        const float tmp = cs[i];
+        int j;
+        for (j = i; j >= 1 && tmp < cs[j - 1]; j--) cs[j] = cs[j - 1];
+        cs[j] = tmp;
+    }
+    sel = 0;
+    const int top_k = num_valid < kv.prm.top_k ? num_valid : kv.prm.top_k;
+    if (top_k > 0) {
+        float cost = 0.0f;
+        for (int i = 0; i < top_k; ++i) cost += cs[i];
+        const float thr = cs[top_k - 1];
+        for (int i = 0; i < nsrc; ++i)
+            if (cv[i] <= thr) sel |= (1u << i);
+        return cost / (float)top_k;
+    }
+    return 2.0f;
+}
+
+// ComputeGeomConsistencyCost (src/ACMMP.cu:518-543)
+DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
+    const float max_cost = 3.0f;
+    const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
+    const float depth = plane_depth(rc, h, px, py);
+    // Get3DPointonWorld_cu (:480-504)
+    float X[3];
+    X[0] = depth * ((float)px - rc.K[2]) / rc.K[0];
+    X[1] = depth * ((float)py - rc.K[5]) / rc.K[4];
+    X[2] = depth;
+    float Wp[3];
+    Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) +
+            -(rc.R[0] * rc.t[0] + rc.R[3] * rc.t[1] + rc.R[6] * rc.t[2]);
+    Wp[1] = (rc.R[1] * X[0] + rc.R[4] * X[1] + rc.R[7] * X[2]) +
+            -(rc.R[1] * rc.t[0] + rc.R[4] * rc.t[1] + rc.R[7] * rc.t[2]);
+    Wp[2] = (rc.R[2] * X[0] + rc.R[5] * X[1] + rc.R[8] * X[2]) +
+            -(rc.R[2] * rc.t[0] + rc.R[5] * rc.t[1] + rc.R[8] * rc.t[2]);
+    // ProjectonCamera_cu (:506-516)
+    float T[3];
+    T[0] = sc.R[0] * Wp[0] + sc.R[1] * Wp[1] + sc.R[2] * Wp[2] + sc.t[0];
+    T[1] = sc.R[3] * Wp[0] + sc.R[4] * Wp[1] + sc.R[5] * Wp[2] + sc.t[1];
+    T[2] = sc.R[6] * Wp[0] + sc.R[7] * Wp[1] + sc.R[8] * Wp[2] + sc.t[2];
+    const float sd = sc.K[6] * T[0] + sc.K[7] * T[1] + sc.K[8] * T[2];
+    const float sx = (sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2]) / sd;
+    const float sy = (sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2]) / sd;
+    const float src_depth = tex_trunc(kv.dep[v], kv.dpitch[v], kv.dw[v], kv.dh[v], sx, sy);
+    if (src_depth == 0.0f) return max_cost;
+    float Y[3];
+    Y[0] = src_depth * (sx - sc.K[2]) / sc.K[0];
+    Y[1] = src_depth * (sy - sc.K[5]) / sc.K[4];
+    Y[2] = src_depth;
+    float Wq[3];
+    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) +
+            -(sc.R[0] * sc.t[0] + sc.R[3] * sc.t[1] + sc.R[6] * sc.t[2]);
+    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) +
+            -(sc.R[1] * sc.t[0] + sc.R[4] * sc.t[1] + sc.R[7] * sc.t[2]);
+    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) +
+            -(sc.R[2] * sc.t[0] + sc.R[5] * sc.t[1] + sc.R[8] * sc.t[2]);
+    float U[3];
+    U[0] = rc.R[0] * Wq[0] + rc.R[1] * Wq[1] + rc.R[2] * Wq[2] + rc.t[0];
+    U[1] = rc.R[3] * Wq[0] + rc.R[4] * Wq[1] + rc.R[5] * Wq[2] + rc.t[1];
+    U[2] = rc.R[6] * Wq[0] + rc.R[7] * Wq[1] + rc.R[8] * Wq[2] + rc.t[2];
+    const float rd = rc.K[6] * U[0] + rc.K[7] * U[1] + rc.K[8] * U[2];
+    const float bx = (rc.K[0] * U[0] + rc.K[1] * U[1] + rc.K[2] * U[2]) / rd;
+    const float by = (rc.K[3] * U[0] + rc.K[4] * U[1] + rc.K[5] * U[2]) / rd;
+    const float dc = (float)px - bx;
+    const float dr = (float)py - by;
+    const float e = dm_sqrt(dc * dc + dr * dr);
+    return (e < max_cost) ? e : max_cost;
+}
+
+DEV dm_rng make_rng(const KViews &kv, int center, uint32_t phase) {
+    dm_rng g;
+    g.k0 = kv.prm.seed_lo;
+    g.k1 = kv.prm.seed_hi;
+    g.pix = (uint32_t)center;
+    g.phase = phase;
+    g.stream = kv.prm.rng_stream;
+    g.draw = 0;
+    return g;
+}
+
+DEV int cs_index(const KViews &kv, int x, int y) { return y * kv.Wh + (x >> 1); }
+
+// SpatialGauss / RangeGauss (src/ACMMP.cu:151-161), pow(v,2) pinned to v*v.
+DEV float spatial_gauss(float x1, float y1, float x2, float y2, float sigma) {
+    const float dis = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) - 0.0f;
+    return dm_expf((float)(-1.0 * (double)dis / (double)(2 * sigma * sigma)));
+}
+DEV float range_gauss(float x, float sigma) {
+    const float xp = x - 0.0f;
+    return dm_expf((float)(-1.0 * (double)(xp * xp) / (double)(2 * sigma * sigma)));
+}
+
+// upscale_normal (src/ACMMP.cu:548-607)
+DEV float4 upscale_normal(const KViews &kv, const KState &st, int px, int py, float sigmad,
+                          float sigmar, int nn, float o_y, float o_x, float refPix, float &cost_out) {
+    const int scols = (int)kv.prm.scaled_cols, srows = (int)kv.prm.scaled_rows;
+    float c_total = 0.0f, norm = 0.0f;
+    float4 n_total = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int j = -nn; j <= nn; ++j) {
+        int r_y = (int)(o_y + (float)j);
+        r_y = (r_y > 0 ? (r_y < srows ? r_y : srows - 1) : 0);
+        const int r_ys = py + j;
+        for (int i = -nn; i <= nn; ++i) {
+            int r_x = (int)(o_x + (float)i);
+            r_x = (r_x > 0 ? (r_x < scols ? r_x : scols - 1) : 0);
+            const float4 sn = st.scaled[r_y * scols + r_x];
+            const float nb = texel(kv.img[0], kv.ipitch[0], kv.W, kv.H, px + i, r_ys);
+            const float tg = spatial_gauss(o_x, o_y, (float)r_x, (float)r_y, sigmad) *
+                             range_gauss(dm_fabs(refPix - nb), sigmar);
+            norm += tg;
+            c_total += sn.w * tg;
+            n_total.x = n_total.x + sn.x * tg;
+            n_total.y = n_total.y + sn.y * tg;
+            n_total.z = n_total.z + sn.z * tg;
+        }
+    }
+    cost_out = c_total / norm;
+    n_total.x = n_total.x / norm;
+    n_total.y = n_total.y / norm;
+    n_total.z = n_total.z / norm;
+    normalize3(n_total);
+    return n_total;
+}
+
+// ------------------------------------------------------------------ init
+// RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
+// writes the colour-split "current" buffers.
+template <int NS>
+__global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
+    const KViews &kv = *kvp;
+    const int px = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    if (px >= kv.W || py >= kv.H) return;
+    const acmmp_params &prm = kv.prm;
+    const acmmp_camera &c0 = kv.cam[0];
+    const int center = py * kv.W + px;
+    dm_rng rs = make_rng(kv, center, 0u);
+    RefPatch rp;
+    ref_patch(kv, px, py, rp);
+    float4 plane;
+    float cost;
+    uint32_t sel = 0;
+    if (!prm.geom_consistency && !prm.hierarchy && !prm.seeded) {
+        const float depth = dm_rng_uniform(&rs) * (prm.depth_max - prm.depth_min) + prm.depth_min;
+        plane = random_normal(c0, px, py, rs, depth);
+        plane.w = distance_to_origin(c0, px, py, depth, plane);
+        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+    } else if (prm.seeded) {
+        plane = st.seed[center];
+        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+    } else if (prm.planar_prior) {
+        if (st.mask[center] > 0 && st.rm_cost[center] >= 0.1f) {
+            const float perturbation = 0.02f;
+            const float4 h = st.prior[center];
+            float dp = h.w;
+            const float dmin = (1 - 3 * perturbation) * dp;
+            const float dmax = (1 + 3 * perturbation) * dp;
+            dp = dm_rng_uniform(&rs) * (dmax - dmin) + dmin;
+            plane = perturbed_normal(c0, px, py, h, rs, kv.pert3_pi);
+            plane.w = dp;
+        } else {
+            plane = st.rm_plane[center];
+            plane.w = distance_to_origin(c0, px, py, plane.w, plane);
+        }
+        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+    } else if (prm.upsample) {
+        const float scale = (float)(1.0 * (double)prm.scaled_cols / (double)kv.W);
+        const float sigmad = 0.50f, sigmar = 25.5f;
+        const float a = (float)kv.W / prm.scaled_cols, b = (float)kv.H / prm.scaled_rows;
+        const int Imagescale = (int)(a > b ? a : b);
+        const int nn = (Imagescale * Imagescale + 1) / 2;
+        const float o_y = (float)py * scale, o_x = (float)px * scale;
+        const float refPix = texel(kv.img[0], kv.ipitch[0], kv.W, kv.H, px, py);
+        float ucost;
+        const float4 n_total = upscale_normal(kv, st, px, py, sigmad, sigmar, nn, o_y, o_x, refPix, ucost);
+        const float4 prev = st.rm_plane[center];
+        const float c_pre = initial_cost<NS>(kv, rp, px, py, prev, sel);
+        st.pre_cost[center] = c_pre;
+        plane = to_cam(c0, n_total);
+        plane.w = distance_to_origin(c0, px, py, prev.w, plane);
+        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+    } else {
+        float4 h = prm.hierarchy ? st.scaled[center] : st.rm_plane[center];
+        h = to_cam(c0, h);
+        h.w = distance_to_origin(c0, px, py, h.w, h);
+        plane = h;
+        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+    }
+    const int c = (px + py) & 1;
+    const int ci = cs_index(kv, px, py);
+    st.plane[c][ci] = plane;
+    st.cost[c][ci] = cost;
+    st.sv[c][ci] = sel;
+}
+
+// ------------------------------------------------------------- the sweep
+// CheckerboardPropagation (src/ACMMP.cu:786-1173) for the pixels of one colour.
+// Lane (k, y) -> pixel x = 2k + ((y + colour) & 1). Neighbour state is read
+// from the colour-split "current" buffers (the half-sweep snapshot); own state
+// is kept in registers and written to the "next" buffer of this colour.
+template <int NS>
+__global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
+                                               int iter) {
+    const KViews &kv = *kvp;
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    const int width = kv.W, height = kv.H;
+    if (py >= height) return;
+    const int px = 2 * k + ((py + colour) & 1);
+    if (px >= width) return;
+    const int oc = colour ^ 1;
+    const int my = cs_index(kv, px, py);
+    const float4 *plane_same = st.plane[colour];
+    const float4 *plane_opp = st.plane[oc];
+    const float *cost_same = st.cost[colour];
+    const float *cost_opp = st.cost[oc];
+    float4 my_plane = plane_same[my];
+    float my_cost = cost_same[my];
+    uint32_t my_sv = st.sv[colour][my];
+    if (py >= kv.sweep_rows) {  // rows the reference grid never reaches
+        st.plane_nx[colour][my] = my_plane;
+        st.cost_nx[colour][my] = my_cost;
+        return;
+    }
+    const acmmp_params &prm = kv.prm;
+    const acmmp_camera &c0 = kv.cam[0];
+    const int nsrc = kv.nsrc;
+    const int center = py * width + px;
+
+    // ---- adaptive checkerboard sampling (:813-991); positions kept as (x, y)
+    int posx[8], posy[8];
+    bool flag[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) { flag[d] = false; posx[d] = px; posy[d] = py; }
+    float costMin;
+    // up_far (opposite colour)
+    if (py > 2) {
+        flag[1] = true;
+        int by = py - 3;
+        costMin = cost_opp[cs_index(kv, px, by)];
+        for (int i = 1; i < 11; ++i) {
+            if (py > 2 + 2 * i) {
+                const int ty = py - 3 - 2 * i;
+                const float c = cost_opp[cs_index(kv, px, ty)];
+                if (c < costMin) { costMin = c; by = ty; }
+            }
+        }
+        posy[1] = by;
+    }
+    if (py < height - 3) {  // down_far
+        flag[3] = true;
+        int by = py + 3;
+        costMin = cost_opp[cs_index(kv, px, by)];
+        for (int i = 1; i < 11; ++i) {
+            if (py < height - 3 - 2 * i) {
+                const int ty = py + 3 + 2 * i;
+                const float c = cost_opp[cs_index(kv, px, ty)];
+                if (c < costMin) { costMin = c; by = ty; }
+            }
+        }
+        posy[3] = by;
+    }
+    if (px > 2) {  // left_far
+        flag[5] = true;
+        int bx = px - 3;
+        costMin = cost_opp[cs_index(kv, bx, py)];
+        for (int i = 1; i < 11; ++i) {
+            if (px > 2 + 2 * i) {
+                const int tx = px - 3 - 2 * i;
+                const float c = cost_opp[cs_index(kv, tx, py)];
+                if (c < costMin) { costMin = c; bx = tx; }
+            }
+        }
+        posx[5] = bx;
+    }
+    if (px < width - 3) {  // right_far: reversed comparison keeps the max (:879)
+        flag[7] = true;
+        int bx = px + 3;
+        costMin = cost_opp[cs_index(kv, bx, py)];
+        for (int i = 1; i < 11; ++i) {
+            if (px < width - 3 - 2 * i) {
+                const int tx = px + 3 + 2 * i;
+                const float c = cost_opp[cs_index(kv, tx, py)];
+                if (costMin < c) { costMin = c; bx = tx; }
+            }
+        }
+        posx[7] = bx;
+    }
+    // near "V" searches: base point is the opposite colour, the V arms are
+    // the same colour (read from the snapshot).
+    if (py > 0) {  // up_near
+        flag[0] = true;
+        int bx = px, by = py - 1;
+        costMin = cost_opp[cs_index(kv, bx, by)];
+        for (int i = 0; i < 3; ++i) {
+            const int ty = py - 2 - i;
+            if (py > 1 + i && px > i) {
+                const float c = cost_same[cs_index(kv, px - i, ty)];
+                if (c < costMin) { costMin = c; bx = px - i; by = ty; }
+            }
+            if (py > 1 + i && px < width - 1 - i) {
+                const float c = cost_same[cs_index(kv, px + i, ty)];
+                if (c < costMin) { costMin = c; bx = px + i; by = ty; }
+            }
+        }
+        posx[0] = bx; posy[0] = by;
+    }
+    if (py < height - 1) {  // down_near
+        flag[2] = true;
+        int bx = px, by = py + 1;
+        costMin = cost_opp[cs_index(kv, bx, by)];
+        for (int i = 0; i < 3; ++i) {
+            const int ty = py + 2 + i;
+            if (py < height - 2 - i && px > i) {
+                const float c = cost_same[cs_index(kv, px - i, ty)];
+                if (c < costMin) { costMin = c; bx = px - i; by = ty; }
+            }
+            if (py < height - 2 - i && px < width - 1 - i) {
+                const float c = cost_same[cs_index(kv, px + i, ty)];
+                if (c < costMin) { costMin = c; bx = px + i; by = ty; }
+            }
+        }
+        posx[2] = bx; posy[2] = by;
+    }
+    if (px > 0) {  // left_near
+        flag[4] = true;
+        int bx = px - 1, by = py;
+        costMin = cost_opp[cs_index(kv, bx, by)];
+        for (int i = 0; i < 3; ++i) {
+            const int tx = px - 2 - i;
+            if (px > 1 + i && py > i) {
+                const float c = cost_same[cs_index(kv, tx, py - i)];
+                if (c < costMin) { costMin = c; bx = tx; by = py - i; }
+            }
+            if (px > 1 + i && py < height - 1 - i) {
+                const float c = cost_same[cs_index(kv, tx, py + i)];
+                if (c < costMin) { costMin = c; bx = tx; by = py + i; }
+            }
+        }
+        posx[4] = bx; posy[4] = by;
+    }
+    if (px < width - 1) {  // right_near
+        flag[6] = true;
+        int bx = px + 1, by = py;
+        costMin = cost_opp[cs_index(kv, bx, by)];
+        for (int i = 0; i < 3; ++i) {
+            const int tx = px + 2 + i;
+            if (px < width - 2 - i && py > i) {
+                const float c = cost_same[cs_index(kv, tx, py - i)];
+                if (c < costMin) { costMin = c; bx = tx; by = py - i; }
+            }
+            if (px < width - 2 - i && py < height - 1 - i) {
+                const float c = cost_same[cs_index(kv, tx, py + i)];
+                if (c < costMin) { costMin = c; bx = tx; by = py + i; }
+            }
+        }
+        posx[6] = bx; posy[6] = by;
+    }
+    float4 cand[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const int qx = posx[d], qy = posy[d];
+        const float4 *src = (((qx + qy) & 1) == colour) ? plane_same : plane_opp;
+        cand[d] = flag[d] ? src[cs_index(kv, qx, qy)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+    RefPatch rp;
+    ref_patch(kv, px, py, rp);
+
+    // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
+    float cost_array[8][NS];
+    for (int d = 0; d < 8; ++d) {
+        if (flag[d]) {
+            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = bilateral_ncc(kv, rp, v + 1, px, py, cand[d]);
+        } else {
+            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = (d == 0 && v == 0) ? 2.0f : 0.0f;
+        }
+    }
+
+    // ---- multi-hypothesis joint view selection (:994-1056)
+    float vsp[NS];
+    for (int j = 0; j < nsrc; ++j) vsp[j] = 0.0f;
+    {
+        const uint32_t *sv_opp = st.sv[oc];
+        uint32_t nb[4];
+        nb[0] = (py > 0) ? sv_opp[cs_index(kv, px, py - 1)] : 0u;
+        nb[1] = (py < height - 1) ? sv_opp[cs_index(kv, px, py + 1)] : 0u;
+        nb[2] = (px > 0) ? sv_opp[cs_index(kv, px - 1, py)] : 0u;
+        nb[3] = (px < width - 1) ? sv_opp[cs_index(kv, px + 1, py)] : 0u;
+        for (int i = 0; i < 4; ++i) {
+            if (flag[2 * i]) {
+                for (int j = 0; j < nsrc; ++j) vsp[j] += ((nb[i] >> j) & 1u) ? 0.9f : 0.1f;
+            }
+        }
+    }
+    float probs[NS];
+    const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
+    for (int i = 0; i < nsrc; i++) {
+        float count = 0;
+        int count_false = 0;
+        float tmpw = 0;
+        for (int j = 0; j < 8; j++) {
+            const float c = cost_array[j][i];
+            if (c < cost_threshold) {
+                tmpw += dm_expf(c * c / (-0.18f));
+                count++;
+            }
+            if (c > 1.2f) count_false++;
+        }
+        float pr = 0.0f;
+        if (count > 2 && count_false < 3) pr = tmpw / count;
+        else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
+        probs[i] = pr * vsp[i];
+    }
+    {  // TransformPDFToCDF (:107-121)
+        float sum = 0.0f;
+        for (int i = 0; i < nsrc; ++i) sum += probs[i];
+        const float inv = 1.0f / sum;
+        float cum = 0.0f;
+        for (int i = 0; i < nsrc; ++i) {
+            cum += probs[i] * inv;
+            probs[i] = cum;
+        }
+    }
+    dm_rng rs = make_rng(kv, center, 1u + (uint32_t)iter);
+    float view_weights[NS];
+    for (int j = 0; j < nsrc; ++j) view_weights[j] = 0.0f;
+    for (int sample = 0; sample < 15; ++sample) {
+        const float rand_prob = dm_rng_uniform(&rs) - FLT_EPSILON;
+        for (int image_id = 0; image_id < nsrc; ++image_id) {
+            if (probs[image_id] > rand_prob) { view_weights[image_id] += 1.0f; break; }
+        }
+    }
+    uint32_t temp_sv = 0;
+    float weight_norm = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        if (view_weights[i] > 0) { temp_sv |= (1u << i); weight_norm += view_weights[i]; }
+    }
+
+    float final_costs[8];
+    for (int i = 0; i < 8; ++i) {
+        float fc = 0.0f;
+        for (int j = 0; j < nsrc; ++j) {
+            if (view_weights[j] > 0) {
+                if (prm.geom_consistency) {
+                    if (flag[i]) fc += view_weights[j] * (cost_array[i][j] + 0.2f * geom_cost(kv, j + 1, cand[i], px, py));
+                    else fc += view_weights[j] * (cost_array[i][j] + 0.1f * 3.0f);
+                } else {
+                    fc += view_weights[j] * cost_array[i][j];
+                }
+            }
+        }
+        final_costs[i] = fc / weight_norm;
+    }
+    int min_cost_idx = 0;
+    {
+        float m = final_costs[0];
+        for (int i = 1; i < 8; ++i)
+            if (final_costs[i] <= m) { m = final_costs[i]; min_cost_idx = i; }
+    }
+
+    // ---- current hypothesis (:1080-1093) + refinement (:707-784): one NCC
+    // site. t = 0 evaluates the current plane; t = 1..5 the refinement planes.
+    const bool has_prior = prm.planar_prior && st.mask[center] > 0;
+    float4 prior_plane = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (prm.planar_prior) prior_plane = st.prior[center];
+    float cost_now = 0.0f, depth_now = 0.0f, restricted_cost = 0.0f, depth_prior = 0.0f;
+    float4 plane_now = my_plane;
+    float ref_depths[5];
+    float4 ref_normals[5];
+    const float gamma = 0.5f;
+    const float depth_sigma = (prm.depth_max - prm.depth_min) / 64.0f;
+    const float two_dss = 2 * depth_sigma * depth_sigma;
+    const float two_ass = 2 * kv.angle_sigma * kv.angle_sigma;
+    const float beta = 0.18f;
+
+    for (int t = 0; t < 6; ++t) {
+        float4 h;
+        if (t == 0) {
+            h = my_plane;
+        } else {
+            h = ref_normals[t - 1];
+            h.w = distance_to_origin(c0, px, py, ref_depths[t - 1], h);
+        }
+        float tc = 0.0f;
+        for (int j = 0; j < nsrc; ++j) {
+            if (view_weights[j] > 0) {
+                const float c = bilateral_ncc(kv, rp, j + 1, px, py, h);
+                if (prm.geom_consistency) tc += view_weights[j] * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
+                else tc += view_weights[j] * c;
+            }
+        }
+        tc /= weight_norm;
+        if (t == 0) {
+            cost_now = tc;
+            my_cost = cost_now;  // costs[center] = cost_now (:1092)
+            depth_now = plane_depth(c0, my_plane, px, py);
+            if (prm.planar_prior) {
+                depth_prior = plane_depth(c0, prior_plane, px, py);
+                if (st.mask[center] > 0) {
+                    float rfc[8];
+                    for (int i = 0; i < 8; i++) {
+                        rfc[i] = 0.0f;
+                        if (flag[i]) {
+                            const float dn = plane_depth(c0, cand[i], px, py);
+                            const float dd = dn - depth_prior;
+                            const float ad = dm_acosf(dot3(prior_plane, cand[i]));
+                            const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
+                            rfc[i] = dm_expf(-final_costs[i] * final_costs[i] / beta) * prior;
+                        }
+                    }
+                    int max_idx = 0;
+                    {
+                        float m = rfc[0];
+                        for (int i = 1; i < 8; ++i)
+                            if (rfc[i] >= m) { m = rfc[i]; max_idx = i; }
+                    }
+                    const float dn = plane_depth(c0, my_plane, px, py);
+                    const float dd = dn - depth_prior;
+                    const float ad = dm_acosf(dot3(prior_plane, my_plane));
+                    const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
+                    const float rcn = dm_expf(-cost_now * cost_now / beta) * prior;
+                    if (flag[max_idx]) {
+                        const float db = plane_depth(c0, cand[max_idx], px, py);
+                        if (db >= prm.depth_min && db <= prm.depth_max && rfc[max_idx] > rcn) {
+                            // the reference assigns a shadowing local here (:1119/:1130):
+                            // the outer depth_now is NOT updated
+                            my_plane = cand[max_idx];
+                            my_cost = final_costs[max_idx];
+                            restricted_cost = rfc[max_idx];
+                            my_sv = temp_sv;
+                        }
+                    }
+                } else if (flag[min_cost_idx]) {
+                    const float db = plane_depth(c0, cand[min_cost_idx], px, py);
+                    if (db >= prm.depth_min && db <= prm.depth_max && final_costs[min_cost_idx] < cost_now) {
+                        depth_now = db;
+                        my_plane = cand[min_cost_idx];
+                        my_cost = final_costs[min_cost_idx];
+                    }
+                }
+            }
+            plane_now = my_plane;  // pin A3
+            if (!prm.planar_prior && flag[min_cost_idx]) {
+                const float db = plane_depth(c0, cand[min_cost_idx], px, py);
+                if (db >= prm.depth_min && db <= prm.depth_max && final_costs[min_cost_idx] < cost_now) {
+                    depth_now = db;
+                    plane_now = cand[min_cost_idx];
+                    cost_now = final_costs[min_cost_idx];
+                    my_sv = temp_sv;
+                }
+            }
+            // PlaneHypothesisRefinement: candidate generation (:718-741)
+            float depth_rand;
+            float4 plane_rand;
+            if (has_prior) {
+                const float dpri = plane_depth(c0, prior_plane, px, py);
+                depth_prior = dpri;
+                depth_rand = dm_rng_uniform(&rs) * 6 * depth_sigma + (dpri - 3 * depth_sigma);
+                plane_rand = perturbed_normal(c0, px, py, prior_plane, rs, kv.angle_sigma);
+            } else {
+                depth_rand = dm_rng_uniform(&rs) * (prm.depth_max - prm.depth_min) + prm.depth_min;
+                plane_rand = random_normal(c0, px, py, rs, depth_now);
+            }
+            const float perturbation = 0.02f;
+            float depth_perturbed = depth_now;
+            const float dmin_p = (1 - perturbation) * depth_perturbed;
+            const float dmax_p = (1 + perturbation) * depth_perturbed;
+            do {
+                depth_perturbed = dm_rng_uniform(&rs) * (dmax_p - dmin_p) + dmin_p;
+            } while (depth_perturbed < prm.depth_min && depth_perturbed > prm.depth_max);
+            const float4 plane_perturbed = perturbed_normal(c0, px, py, plane_now, rs, kv.pert_pi);
+            ref_depths[0] = depth_rand; ref_normals[0] = plane_now;
+            ref_depths[1] = depth_now;  ref_normals[1] = plane_rand;
+            ref_depths[2] = depth_rand; ref_normals[2] = plane_rand;
+            ref_depths[3] = depth_now;  ref_normals[3] = plane_perturbed;
+            ref_depths[4] = depth_perturbed; ref_normals[4] = plane_now;
+        } else {
+            const float depth_before = plane_depth(c0, h, px, py);
+            if (has_prior) {
+                const float dd = ref_depths[t - 1] - depth_prior;
+                const float ad = dm_acosf(dot3(prior_plane, h));
+                const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
+                const float rtc = dm_expf(-tc * tc / beta) * prior;
+                if (depth_before >= prm.depth_min && depth_before <= prm.depth_max && rtc > restricted_cost) {
+                    depth_now = depth_before;
+                    plane_now = h;
+                    cost_now = tc;
+                    restricted_cost = rtc;
+                }
+            } else {
+                if (depth_before >= prm.depth_min && depth_before <= prm.depth_max && tc < cost_now) {
+                    depth_now = depth_before;
+                    plane_now = h;
+                    cost_now = tc;
+                }
+            }
+        }
+    }
+    // hierarchy gate (:1163-1172)
+    if (prm.hierarchy) {
+        if (cost_now < st.pre_cost[center] - 0.1f) {
+            my_cost = cost_now;
+            my_plane = plane_now;
+        }
+    } else {
+        my_cost = cost_now;
+        my_plane = plane_now;
+    }
+    st.plane_nx[colour][my] = my_plane;
+    st.cost_nx[colour][my] = my_cost;
+    st.sv[colour][my] = my_sv;
+}
+
+// GetDepthandNormal (src/ACMMP.cu:1199-1212) fused with the colour-split ->
+// row-major conversion.
+__global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
+    const KViews &kv = *kvp;
+    const int px = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    if (px >= kv.W || py >= kv.H) return;
+    const int c = (px + py) & 1;
+    const int ci = cs_index(kv, px, py);
+    float4 h = st.plane[c][ci];
+    h.w = plane_depth(kv.cam[0], h, px, py);
+    h = to_world(kv.cam[0], h);
+    const int center = py * kv.W + px;
+    st.rm_plane[center] = h;
+    st.rm_cost[center] = st.cost[c][ci];
+    st.rm_sv[center] = st.sv[c][ci];
+}
+
+// CheckerboardFilter (src/ACMMP.cu:1214-1328) on one colour, in place on the
+// row-major planes: every read is of the opposite colour.
+__global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, KState st, int colour) {
+    const KViews &kv = *kvp;
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    const int width = kv.W, height = kv.H;
+    if (py >= kv.sweep_rows) return;
+    const int px = 2 * k + ((py + colour) & 1);
+    if (px >= width) return;
+    float4 *ph = st.rm_plane;
+    const int center = py * width + px;
+    if (st.rm_cost[center] < 0.001f) return;
+    float f[21];
+    int n = 0;
+    f[n++] = ph[center].w;
+    const int left = center - 1, leftleft = center - 3;
+    const int up = center - width, upup = center - 3 * width;
+    const int down = center + width, downdown = center + 3 * width;
+    const int right = center + 1, rightright = center + 3;
+    if (py > 0) f[n++] = ph[up].w;
+    if (py > 2) f[n++] = ph[upup].w;
+    if (py > 4) f[n++] = ph[upup - width * 2].w;
+    if (py < height - 1) f[n++] = ph[down].w;
+    if (py < height - 3) f[n++] = ph[downdown].w;
+    if (py < height - 5) f[n++] = ph[downdown + width * 2].w;
+    if (px > 0) f[n++] = ph[left].w;
+    if (px > 2) f[n++] = ph[leftleft].w;
+    if (px > 4) f[n++] = ph[leftleft - 2].w;
+    if (px < width - 1) f[n++] = ph[right].w;
+    if (px < width - 3) f[n++] = ph[rightright].w;
+    if (px < width - 5) f[n++] = ph[rightright + 2].w;
+    if (py > 0 && px < width - 2) f[n++] = ph[up + 2].w;
+    if (py < height - 1 && px < width - 2) f[n++] = ph[down + 2].w;
+    if (py > 0 && px > 1) f[n++] = ph[up - 2].w;
+    if (py < height - 1 && px > 1) f[n++] = ph[down - 2].w;
+    if (px > 0 && py > 2) f[n++] = ph[left - width * 2].w;
+    if (px < width - 1 && py > 2) f[n++] = ph[right - width * 2].w;
+    if (px > 0 && py < height - 2) f[n++] = ph[left + width * 2].w;
+    if (px < width - 1 && py < height - 2) f[n++] = ph[right + width * 2].w;
+    for (int i = 1; i < n; i++) {  // sort_small
+        const float tmp = f[i];
+        int j;
+        for (j = i; j >= 1 && tmp < f[j - 1]; j--) f[j] = f[j - 1];
+        f[j] = tmp;
+    }
+    const int m = n / 2;
+    ph[center].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
+}
+
+// T1 kernel: costs of a given plane per pixel against every source view.
+template <int NS>
+__global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
+                                                    float *out, float *out_init, uint32_t *out_views) {
+    const KViews &kv = *kvp;
+    const int px = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    if (px >= kv.W || py >= kv.H) return;
+    const int c = py * kv.W + px;
+    RefPatch rp;
+    ref_patch(kv, px, py, rp);
+    const float4 h = planes[c];
+    if (out)
+        for (int v = 0; v < kv.nsrc; ++v) out[(size_t)c * kv.nsrc + v] = bilateral_ncc(kv, rp, v + 1, px, py, h);
+    if (out_init) {
+        uint32_t sel = 0;
+        out_init[c] = initial_cost<NS>(kv, rp, px, py, h, sel);
+        if (out_views) out_views[c] = sel;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kvp, const float4 *planes,
+                                                   float *out) {
+    const KViews &kv = *kvp;
+    const int px = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
+    if (px >= kv.W || py >= kv.H) return;
+    const int c = py * kv.W + px;
+    for (int v = 0; v < kv.nsrc; ++v) out[(size_t)c * kv.nsrc + v] = geom_cost(kv, v + 1, planes[c], px, py);
+}
+
+// ---------------------------------------------------------------- launchers
+// Source-view count -> array capacity of the templated kernels.
+static int ns_bucket(int nsrc) {
+    if (nsrc <= 4) return 4;
+    if (nsrc <= 9) return 9;
+    if (nsrc <= 16) return 16;
+    if (nsrc <= 20) return 20;
+    return 32;
+}
+
+#define ACMMP_DISPATCH_NS(nsrc, KERNEL, ...)                  \
+    switch (ns_bucket(nsrc)) {                                \
+        case 4: KERNEL<4><<<__VA_ARGS__>>>; break;            \
+        case 9: KERNEL<9><<<__VA_ARGS__>>>; break;            \
+        case 16: KERNEL<16><<<__VA_ARGS__>>>; break;          \
+        case 20: KERNEL<20><<<__VA_ARGS__>>>; break;          \
+        default: KERNEL<32><<<__VA_ARGS__>>>; break;          \
+    }
+
+hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
+    switch (ns_bucket(h_kv.nsrc)) {
+        case 4: k_init<4><<<grid, block, 0, stream>>>(d_kv, st); break;
+        case 9: k_init<9><<<grid, block, 0, stream>>>(d_kv, st); break;
+        case 16: k_init<16><<<grid, block, 0, stream>>>(d_kv, st); break;
+        case 20: k_init<20><<<grid, block, 0, stream>>>(d_kv, st); break;
+        default: k_init<32><<<grid, block, 0, stream>>>(d_kv, st); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
+                        hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.Wh + 63) / 64, (h_kv.H + 3) / 4);
+    switch (ns_bucket(h_kv.nsrc)) {
+        case 4: k_sweep<4><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
+        case 9: k_sweep<9><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
+        case 16: k_sweep<16><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
+        case 20: k_sweep<20><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
+        default: k_sweep<32><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
+    k_finalize<<<grid, block, 0, stream>>>(d_kv, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                         hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.Wh + 63) / 64, (h_kv.H + 3) / 4);
+    k_filter<<<grid, block, 0, stream>>>(d_kv, st, colour);
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float4 *planes, float *out,
+                             float *out_init, uint32_t *out_views, hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
+    switch (ns_bucket(h_kv.nsrc)) {
+        case 4: k_eval_costs<4><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
+        case 9: k_eval_costs<9><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
+        case 16: k_eval_costs<16><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
+        case 20: k_eval_costs<20><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
+        default: k_eval_costs<32><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4 *planes, float *out,
+                            hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
+    k_eval_geom<<<grid, block, 0, stream>>>(d_kv, planes, out);
+    return hipGetLastError();
+}
+
+}  // namespace acmmp

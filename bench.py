@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""PatchMatch throughput benchmark (BASELINE.json metric) on 1..N MI355X.
+
+Workload (BASELINE.json configs[1], "cfg2"): per GPU, 10 reference views at
+1600x1200, each with its 9 nearest source views (N = 10 images per problem),
+8 PatchMatch iterations, a photometric pass over the GPU's views, an RCCL
+all-gather of the depth maps, then a geometric-consistency pass over the same
+views (it reads the neighbours' depth maps: the real exchange step).
+
+One "step" = photometric pass + all-gather + geometric pass. Views shard one
+contiguous block of 10 per rank on a 10*N-view arc (weak scaling: per-GPU work
+fixed); boundary views read depth maps produced on neighbouring ranks.
+Inputs are rendered straight into HBM before timing (synthetic, seeded).
+
+value = total pixels processed by all ranks (2 passes x views x W x H) /
+max-over-ranks wall time of the K timed steps, in Mpix/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+BASELINE_METRIC = "Mpixels/sec PatchMatch (1600×1200, 8 iters) at 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_pixel_iter(num_images: int, geom: bool) -> int:
+    """SURVEY §8d / BASELINE.md §3 gather-byte model per pixel-iteration:
+    14*(N-1) NCC calls x 724 B + 572 B of state, + 14*(N-1)*4 B in geometric
+    passes."""
+    b = 14 * (num_images - 1) * 724 + 572
+    if geom:
+        b += 14 * (num_images - 1) * 4
+    return b
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--views", type=int, default=10, help="reference views per GPU")
+    ap.add_argument("--nsrc", type=int, default=9)
+    ap.add_argument("--width", type=int, default=1600)
+    ap.add_argument("--height", type=int, default=1200)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="400x300", help="ref-view crop timed on the CPU oracle")
+    ap.add_argument("--profile-dir", default=None, help="write per-run timing JSON here")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    from acmmp_amd import ACMMP, default_params, scene
+
+    V = args.views * world
+    W, H = args.width, args.height
+    setup = scene.scene_setup(num_views=V, width=W, height=H)
+    mine = list(range(rank * args.views, (rank + 1) * args.views))
+    srcs = {v: setup.pairs[v][:args.nsrc] for v in mine}
+    needed = sorted(set(mine) | {s for v in mine for s in srcs[v]})
+    images = {i: scene.render_torch(setup, i, device) for i in needed}
+    cams = {i: setup.camera(i) for i in needed}
+    torch.cuda.synchronize()
+
+    n_img = 1 + args.nsrc
+    planes = torch.empty((args.views, H, W, 4), dtype=torch.float32, device=device)
+    costs = torch.empty((args.views, H, W), dtype=torch.float32, device=device)
+    my_depth = torch.empty((args.views, H, W), dtype=torch.float32, device=device)
+    all_depth = torch.empty((V, H, W), dtype=torch.float32, device=device) if world > 1 else my_depth
+
+    eng = ACMMP(local_rank)
+    eng.set_timing(True)
+    base = default_params()
+    base.max_iterations = args.iters
+
+    sweep_stats = {"photo": [0.0, 0], "geom": [0.0, 0]}
+
+    def run_view(k: int, v: int, geom: bool):
+        ids = [v] + srcs[v]
+        eng.set_params(base)
+        eng.set_images_device([cams[i] for i in ids], [images[i].data_ptr() for i in ids])
+        if geom:
+            p = eng.params
+            p.geom_consistency = 1
+            p.max_iterations = args.iters  # BASELINE cfg2: 8 iterations in both passes
+            eng.set_params(p)
+            # world == 1: all_depth is my_depth and view ids are 0..views-1
+            eng.set_depth_maps_device([all_depth[i].data_ptr() for i in ids])
+            eng.set_plane_hypotheses_device(planes[k].data_ptr(), costs[k].data_ptr())
+        eng.run_async()
+        if not geom:
+            eng.export_results(planes[k].data_ptr(), costs[k].data_ptr(), my_depth[k].data_ptr())
+        eng.synchronize()
+        t = eng.timing()
+        st = sweep_stats["geom" if geom else "photo"]
+        st[0] += t["sweep_ms"]
+        st[1] += t["sweep_launches"]
+
+    if world == 1:
+        # a single GPU must own every source view of the geometric pass
+        assert all(s in mine for v in mine for s in srcs[v])
+
+    def step():
+        for k, v in enumerate(mine):
+            run_view(k, v, geom=False)
+        if world > 1:
+            dist.all_gather_into_tensor(all_depth, my_depth)
+            torch.cuda.synchronize()
+        for k, v in enumerate(mine):
+            run_view(k, v, geom=True)
+
+    for _ in range(args.warmup):
+        step()
+    for st in sweep_stats.values():
+        st[0], st[1] = 0.0, 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    pix_total = 2 * args.views * world * W * H * args.steps
+    value = pix_total / elapsed / 1e6
+    # roofline of the dominant kernel (k_sweep), timed with hipEvents on the
+    # engine stream: algorithmic bytes per launch / mean launch time
+    P = W * H
+    bytes_photo = (P / 2) * algorithmic_bytes_per_pixel_iter(n_img, False) * sweep_stats["photo"][1]
+    bytes_geom = (P / 2) * algorithmic_bytes_per_pixel_iter(n_img, True) * sweep_stats["geom"][1]
+    sweep_ms = sweep_stats["photo"][0] + sweep_stats["geom"][0]
+    launches = sweep_stats["photo"][1] + sweep_stats["geom"][1]
+    achieved = (bytes_photo + bytes_geom) / (sweep_ms / 1e3) / 1e9 if sweep_ms > 0 else 0.0
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_sweep.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("width") == W and pmc.get("height") == H and pmc.get("num_images") == n_img:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": BASELINE_METRIC,
+        "value": round(value, 4),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded analytic scene rendered into HBM; no DTU data offline)",
+        "config": {
+            "workload": f"cfg2: {args.views} ref views/GPU at {W}x{H}, {n_img} images/problem, "
+                        f"{args.iters} iters, photometric + RCCL depth all-gather + geometric pass",
+            "views_per_gpu": args.views,
+            "width": W,
+            "height": H,
+            "num_images": n_img,
+            "iters": args.iters,
+            "parallelism": f"view-parallel x{world} (one process per GPU, RCCL all-gather of depth maps)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_sweep (CheckerboardPropagation)",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "model": "gather-byte model, SURVEY §8d: B_iter = 14*(N-1)*724 + 572 (+14*(N-1)*4 geom) "
+                     "bytes per pixel-iteration, P/2 pixels per launch",
+            "sweep_launches": launches,
+            "mean_launch_ms": round(sweep_ms / max(launches, 1), 3),
+        },
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, setup, images, cams, srcs, mine)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, setup, images, cams, srcs, mine):
+    """CPU oracle (oracle/acmmp_oracle.c, OpenMP) timed on a bounded sample of
+    the same workload: a crop of the first reference view (principal point
+    shifted) against its full-size source views, photometric, same iterations.
+    Per-pixel work equals the full run's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: baseline leg only
+    from acmmp_amd import default_params
+    from acmmp_amd._abi import Camera
+
+    cw, ch = (int(v) for v in args.cpu_sample.split("x"))
+    v = mine[0]
+    ids = [v] + srcs[v]
+    imgs = [images[i].cpu().numpy() for i in ids]
+    cs = [cams[i] for i in ids]
+    x0 = (args.width - cw) // 2
+    y0 = (args.height - ch) // 2
+    ref = Camera.from_buffer_copy(bytes(cs[0]))
+    ref.K[2] = cs[0].K[2] - x0
+    ref.K[5] = cs[0].K[5] - y0
+    ref.width, ref.height = cw, ch
+    imgs[0] = np.ascontiguousarray(imgs[0][y0:y0 + ch, x0:x0 + cw])
+    cs = [ref] + cs[1:]
+    p = default_params()
+    p.max_iterations = args.iters
+    p.depth_min = cs[0].depth_min * 0.6
+    p.depth_max = cs[0].depth_max * 1.2
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    oracle.build()
+    t0 = time.perf_counter()
+    oracle.run_patchmatch(p, cs, imgs, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(cw * ch / dt / 1e6, 5),
+        "unit": "Mpix/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{cw}x{ch} crop of ref view {v} (K shifted) vs {len(ids) - 1} full {args.width}x{args.height} "
+                  f"source views, {args.iters} iters, photometric, {dt:.2f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,235 @@
+/*
+ * acmmp.h — C-ABI of the MI355X-native ACMMP PatchMatch engine (libacmmp_amd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path, `ACMMP::RunPatchMatch`
+ * (src/ACMMP.cu:1378-1456) and the class surface around it (src/ACMMP.h:58-124).
+ * Every entry point below names the reference member / function it replaces.
+ * Plain C: POD structs, raw pointers + sizes, status-code returns, no exceptions,
+ * no exit(): the reference's CUDA_SAFE_CALL -> exit(EXIT_FAILURE)
+ * (src/ACMMP.cpp:67-75) becomes a negative status + acmmp_last_error().
+ *
+ * Image / map layout (host side): row-major float32, one array per view, size
+ * height*width (the reference's cv::Mat_<float>). Plane hypotheses: row-major
+ * float4 (x, y, z, w) = 4 floats per pixel, exactly the reference's
+ * `float4 *plane_hypotheses_host` (src/ACMMP.h:97).
+ */
+#ifndef ACMMP_H_
+#define ACMMP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACMMP_MAX_IMAGES 33   /* ref + up to 32 sources: the reference's unsigned
+                                 selected_views bitmask and [32] arrays
+                                 (src/ACMMP.cu:437, :805) */
+
+/* Status codes */
+#define ACMMP_OK 0
+#define ACMMP_ERR_ARG -1
+#define ACMMP_ERR_STATE -2
+#define ACMMP_ERR_HIP -3
+#define ACMMP_ERR_IO -4
+#define ACMMP_ERR_UNSUPPORTED -5
+
+/* == struct Camera (src/acmmp_definitions.h:47-55): K, R, t row-major, t is
+ * world->camera, 100 bytes. */
+typedef struct acmmp_camera {
+    float K[9];
+    float R[9];
+    float t[3];
+    int32_t height;
+    int32_t width;
+    float depth_min;
+    float depth_max;
+} acmmp_camera;
+
+/* == struct PatchMatchParams (src/ACMMP.h:32-56) + the pinned RNG key.
+ * Booleans are int32 for ABI stability. Defaults: acmmp_default_params(). */
+typedef struct acmmp_params {
+    int32_t max_iterations;     /* 2 in this fork (src/ACMMP.h:33) */
+    int32_t patch_size;         /* 11 */
+    int32_t num_images;         /* set by the image setters */
+    int32_t max_image_size;     /* 3200 */
+    int32_t radius_increment;   /* 2 */
+    float sigma_spatial;        /* 5 */
+    float sigma_color;          /* 3 */
+    int32_t top_k;              /* 4 */
+    float baseline;             /* 0.54 */
+    float depth_min;
+    float depth_max;
+    float disparity_min;
+    float disparity_max;
+    float scaled_cols;
+    float scaled_rows;
+    int32_t geom_consistency;
+    int32_t planar_prior;
+    int32_t multi_geometry;
+    int32_t hierarchy;
+    int32_t upsample;
+    int32_t seeded;
+    uint32_t seed_lo;           /* Philox key: replaces curand_init(clock64(), ...) */
+    uint32_t seed_hi;           /*   (src/ACMMP.cu:624), see include/acmmp_detmath.h */
+    uint32_t rng_stream;        /* run index: a second RunPatchMatch on the same
+                                   instance re-seeds like the reference's clock64() */
+    int32_t reserved[5];
+} acmmp_params;
+
+/* Per-kernel timing of the last run, measured with hipEvents recorded on the
+ * engine's own stream (enabled by acmmp_set_timing). Milliseconds. */
+typedef struct acmmp_timing {
+    float init_ms;          /* RandomInitialization */
+    float sweep_ms;         /* sum over all Black/Red CheckerboardPropagation launches */
+    int32_t sweep_launches; /* 2 * max_iterations */
+    float finalize_ms;      /* GetDepthandNormal + Black/Red filter */
+    float total_ms;         /* whole RunPatchMatch, device side */
+} acmmp_timing;
+
+typedef struct acmmp_ctx acmmp_ctx;
+
+/* Fills the reference defaults of PatchMatchParams (src/ACMMP.h:32-56). */
+void acmmp_default_params(acmmp_params *p);
+
+/* ~ `ACMMP acmmp;` (src/acmmp_definitions.cpp:260) + cudaSetDevice(0) (:253):
+ * create an engine bound to HIP device `device` with its own stream. */
+int acmmp_create(int device, acmmp_ctx **out);
+/* ~ ACMMP::~ACMMP (src/ACMMP.cpp:109-152). NULL is a no-op. */
+void acmmp_destroy(acmmp_ctx *ctx);
+/* Last error message on this context ("" when none). Never NULL. */
+const char *acmmp_last_error(const acmmp_ctx *ctx);
+
+int acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *p);
+int acmmp_get_params(const acmmp_ctx *ctx, acmmp_params *p);
+
+/* ~ ACMMP::SetGeomConsistencyParams(bool) (src/ACMMP.cpp:447-454): sets
+ * geom_consistency, forces max_iterations = 2, sets multi_geometry if asked. */
+int acmmp_set_geom_consistency_params(acmmp_ctx *ctx, int multi_geometry);
+/* ~ ACMMP::SetPlanarPriorParams (src/ACMMP.cpp:461-464). */
+int acmmp_set_planar_prior_params(acmmp_ctx *ctx);
+/* ~ ACMMP::SetHierarchyParams (src/ACMMP.cpp:456-459). */
+int acmmp_set_hierarchy_params(acmmp_ctx *ctx);
+
+/* In-memory equivalent of InputInitialization + CudaSpaceInitialization
+ * (src/ACMMP.cpp:525-636, :638-681): upload `num_images` grayscale float
+ * images (index 0 = reference view) and their (already rescaled) cameras.
+ * Sets params.num_images and, like InputInitialization (:600-601), derives
+ * depth_min = cams[0].depth_min*0.6, depth_max = cams[0].depth_max*1.2 unless
+ * `keep_depth_range` is non-zero. images[i] has cams[i].height*cams[i].width
+ * floats. Allocates all per-pixel device state for the reference size. */
+int acmmp_set_images(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
+                     const float *const *images, int keep_depth_range);
+
+/* Geometric-consistency inputs (src/ACMMP.cpp:608-635, :683-743): the depth
+ * map of every view (index 0 = ref, i = source i), each sized like that view,
+ * host pointers. */
+int acmmp_set_depth_maps(acmmp_ctx *ctx, const float *const *depths);
+/* Same, BORROWING device buffers already resident on this engine's device
+ * (e.g. slices of an RCCL all-gather): no copy; the caller keeps them alive and
+ * unchanged until the run completes. pitches in floats (NULL = width). */
+int acmmp_set_depth_maps_device(acmmp_ctx *ctx, const float *const *d_depths,
+                                const int32_t *pitches);
+
+/* Zero-copy variant of acmmp_set_images: the engine BORROWS the caller's
+ * device-resident images (row pitch in floats, NULL = width). Inputs stay in
+ * HBM across views and passes; nothing crosses PCIe. */
+int acmmp_set_images_device(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
+                            const float *const *d_images, const int32_t *pitches,
+                            int keep_depth_range);
+
+/* Previous-pass state for the reuse init branch (src/ACMMP.cpp:718-742):
+ * planes = (world-frame normal xyz, depth) float4 per ref pixel, costs per pixel. */
+int acmmp_set_plane_hypotheses(acmmp_ctx *ctx, const float *planes4, const float *costs);
+/* Same from device buffers (copied device-to-device on the engine stream). */
+int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, const float *d_costs);
+
+/* Hierarchy inputs (src/ACMMP.cpp:745-808): low-res scaled planes
+ * (normal xyz + cost-or-depth in w) of size scaled_h*scaled_w, and the
+ * upsampled depth for every ref pixel (plane_hypotheses[center].w, :797-804).
+ * Sets params.upsample using the reference's test (:766), including its
+ * rows/cols swap. */
+int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w,
+                               int scaled_h, const float *upsampled_depth);
+
+/* ~ ACMMP::SetPlanarPrior(unique_ptr<float4>) (src/ACMMP.cpp:476-523): seeded
+ * plane priors, float4 per ref pixel (camera-frame normal, distance). Sets
+ * params.seeded. */
+int acmmp_set_seed_prior(acmmp_ctx *ctx, const float *planes4);
+
+/* ~ ACMMP::CudaPlanarPriorInitialization(vector<float4>, Mat_<float> mask)
+ * (src/ACMMP.cpp:811-831): triangle planes (float4 each) and the per-pixel
+ * triangle label mask (0 = none, k = plane k-1). */
+int acmmp_set_planar_prior(acmmp_ctx *ctx, const float *plane_params4, int num_planes,
+                           const uint32_t *mask);
+
+/* ~ ACMMP::RunPatchMatch (src/ACMMP.cu:1378-1456): init, max_iterations x
+ * (black, red) checkerboard sweeps, depth/normal conversion, black/red median
+ * filter. Results stay resident on the device; then rng_stream += 1. */
+int acmmp_run_patchmatch(acmmp_ctx *ctx);
+/* Asynchronous variant: enqueues the same work on the engine's stream and
+ * returns without synchronising (for multi-view pipelining / benchmarks). */
+int acmmp_run_patchmatch_async(acmmp_ctx *ctx);
+/* Waits for all work enqueued on the engine's stream. */
+int acmmp_synchronize(acmmp_ctx *ctx);
+
+/* Bulk getters replacing the per-pixel GetPlaneHypothesis(int)/GetCost(int)
+ * loops (src/ACMMP.cpp:848-856, src/acmmp_definitions.cpp:287-295).
+ * `n` = capacity in elements (float4 count / float count / u32 count). */
+int acmmp_get_plane_hypotheses(acmmp_ctx *ctx, float *planes4, size_t n);
+int acmmp_get_costs(acmmp_ctx *ctx, float *costs, size_t n);
+int acmmp_get_selected_views(acmmp_ctx *ctx, uint32_t *views, size_t n);
+/* Device-resident result pointers (valid until the next set_images/destroy):
+ * row-major float4 planes (world normal, depth) and float costs. */
+int acmmp_get_device_results(acmmp_ctx *ctx, const float **d_planes4, const float **d_costs);
+
+/* Device-to-device export of the last run's results into caller buffers
+ * (any may be NULL): planes4 (W*H float4), costs (W*H), depth (W*H, the .w
+ * channel — what depths.dmb holds). Enqueued on the engine stream; call
+ * acmmp_synchronize before another stream reads them. */
+int acmmp_export_results(acmmp_ctx *ctx, float *d_planes4, float *d_costs, float *d_depth);
+
+/* ~ GetReferenceImageWidth/Height (src/ACMMP.cpp:833-841), GetCamera (:960-962),
+ * GetMinDepth/GetMaxDepth (:858-866). */
+int acmmp_get_reference_size(const acmmp_ctx *ctx, int *width, int *height);
+int acmmp_get_camera(const acmmp_ctx *ctx, int index, acmmp_camera *cam);
+
+/* Kernel-level evaluation used by the T1 parity tier: for every ref pixel and
+ * the given camera-frame plane hypothesis (float4 per pixel), compute the cost
+ * of every source view (ComputeMultiViewCostVector, src/ACMMP.cu:473-478)
+ * -> out[(y*W+x)*(N-1) + v]; and if out_init is non-NULL the initial cost and
+ * selected-view mask (ComputeMultiViewInitialCostandSelectedViews,
+ * src/ACMMP.cu:434-471). */
+int acmmp_eval_costs(acmmp_ctx *ctx, const float *planes4, float *out_costs,
+                     float *out_init_cost, uint32_t *out_init_views);
+/* ComputeGeomConsistencyCost (src/ACMMP.cu:518-543) for every pixel and view
+ * -> out[(y*W+x)*(N-1) + v]. Needs depth maps. */
+int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out);
+
+/* hipEvent timing of the next runs (on the engine stream). */
+int acmmp_set_timing(acmmp_ctx *ctx, int enable);
+int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
+
+/* Number of visible HIP devices (0 when none / no driver). */
+int acmmp_device_count(void);
+/* Library build string (arch, flags). */
+const char *acmmp_version(void);
+
+/* ---- Reference on-disk formats (src/ACMMP.cpp:154-380,
+ *      src/acmmp_definitions.cpp:179-205). Pure host code. ---- */
+
+/* ReadCamera (src/ACMMP.cpp:154-179). width/height are left 0. */
+int acmmp_read_camera(const char *path, acmmp_camera *cam);
+/* readDepthDmb / readNormalDmb (src/ACMMP.cpp:264-294, :323-353): on success
+ * fills h, w, nb; if data != NULL copies min(cap, h*w*nb) floats. */
+int acmmp_read_dmb(const char *path, int32_t *h, int32_t *w, int32_t *nb, float *data,
+                   size_t cap);
+/* writeDepthDmb / writeNormalDmb (src/ACMMP.cpp:296-321, :355-380). */
+int acmmp_write_dmb(const char *path, int32_t h, int32_t w, int32_t nb, const float *data);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACMMP_H_ */

@@ -1,0 +1,198 @@
+"""GPU (libacmmp_amd.so, gfx950) vs CPU oracle parity — the parity tiers of
+SURVEY §8c, all held to BIT-EXACTNESS (NaN == NaN):
+
+  T1  kernel level: NCC cost vectors, init cost + selected views, geometric
+      consistency cost, for fixed random hypothesis sets;
+  T2  one checkerboard iteration from the same init;
+  T3  end-to-end RunPatchMatch (init, N iterations, depth/normal, filter).
+
+Sizes are small so the oracle finishes in seconds; edge cases follow the
+reference's boundary logic (borders, odd sizes, the skipped last row of the
+checkerboard grid, textureless input -> NaN costs, 1 and 20 source views).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from acmmp_amd import ACMMP, default_params, make_camera, scene
+from parity_util import assert_bit_exact, rel_depth_agreement
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(iters=2, **kw):
+    p = default_params()
+    p.max_iterations = iters
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _random_planes(cams, H, W, seed):
+    """Camera-frame planes (n, d) with n facing the camera, depth in range."""
+    rng = np.random.default_rng(seed)
+    K = np.array(cams[0].K).reshape(3, 3)
+    n = rng.normal(size=(H, W, 3))
+    n[..., 2] = -np.abs(n[..., 2]) - 0.5
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    depth = rng.uniform(400, 800, size=(H, W))
+    ys, xs = np.mgrid[0:H, 0:W]
+    X = np.stack([depth * (xs - K[0, 2]) / K[0, 0], depth * (ys - K[1, 2]) / K[1, 1], depth], -1)
+    d = -(n * X).sum(-1)
+    return np.concatenate([n, d[..., None]], -1).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def small_scene():
+    return scene.make_scene(num_views=10, width=128, height=96)
+
+
+def _gpu_run(p, cams, imgs, depths=None, state=None):
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        if depths is not None:
+            eng.set_depth_maps(depths)
+        if state is not None:
+            eng.set_plane_hypotheses(*state)
+        prm = eng.params
+        eng.RunPatchMatch()
+        return prm, eng.plane_hypotheses(), eng.costs(), eng.selected_views()
+
+
+@pytest.mark.parametrize("nsrc", [1, 4, 9, 20])
+def test_t1_cost_vectors(nsrc):
+    sc = scene.make_scene(num_views=nsrc + 1, width=80, height=60, arc_deg=4.0)
+    cams, imgs = sc.problem(0, nsrc)
+    H, W = imgs[0].shape
+    planes = _random_planes(cams, H, W, seed=nsrc)
+    p = _params()
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        prm = eng.params
+        g_cost, g_init, g_views = eng.eval_costs(planes)
+    r_cost, r_init, r_views = oracle.eval_costs(prm, cams, imgs, planes)
+    assert_bit_exact(g_cost, r_cost, "ncc cost vectors")
+    assert_bit_exact(g_init, r_init, "initial cost")
+    assert_bit_exact(g_views, r_views, "initial selected views")
+    assert (r_cost < 2).mean() > 0.05  # the hypotheses do exercise the full NCC
+
+
+def test_t1_geom_cost(small_scene):
+    cams, imgs = small_scene.problem(0, 4)
+    ids = [0] + small_scene.pairs[0][:4]
+    depths = [small_scene.views[i].depth for i in ids]
+    H, W = imgs[0].shape
+    planes = _random_planes(cams, H, W, seed=3)
+    p = _params(geom_consistency=1)
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        eng.set_depth_maps(depths)
+        prm = eng.params
+        g = eng.eval_geom_costs(planes)
+    r = oracle.eval_geom_costs(prm, cams, imgs, depths, planes)
+    assert_bit_exact(g, r, "geometric consistency cost")
+
+
+@pytest.mark.parametrize("iters", [0, 1])
+def test_t2_init_and_one_sweep(small_scene, iters):
+    cams, imgs = small_scene.problem(0, 9)
+    prm, pl, co, sv = _gpu_run(_params(iters), cams, imgs)
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert_bit_exact(pl, ref["planes"], f"planes after {iters} iterations")
+    assert_bit_exact(co, ref["costs"], "costs")
+    assert_bit_exact(sv, ref["selected_views"], "selected views")
+
+
+def test_t3_photometric_cfg1_shape():
+    """cfg1: 5 views at 400x300, 3 iterations, photometric (the reference's
+    CPU-sized configuration)."""
+    sc = scene.make_scene(num_views=5, width=400, height=300)
+    cams, imgs = sc.problem(2, 4)
+    prm, pl, co, sv = _gpu_run(_params(3), cams, imgs)
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert_bit_exact(pl, ref["planes"], "planes")
+    assert_bit_exact(co, ref["costs"], "costs")
+    assert_bit_exact(sv, ref["selected_views"], "selected views")
+    assert rel_depth_agreement(pl, ref["planes"], ref["costs"]) == 1.0
+    # and the reconstruction is meaningful against the analytic ground truth
+    gt = sc.views[2].depth
+    ok = (gt > 0) & (co < 0.3)
+    rel = np.abs(pl[..., 3] - gt) / np.maximum(gt, 1)
+    assert np.median(rel[ok]) < 0.005
+
+
+def test_t3_geometric_pass(small_scene):
+    """Photometric pass over 4 views, then a geometric pass (Jacobi order)
+    that reads their depth maps, as ProcessProblem does between passes."""
+    V, nsrc = 4, 3
+    outs = {}
+    for ref in range(V):
+        ids = [ref] + [j for j in small_scene.pairs[ref] if j < V][:nsrc]
+        cams = [small_scene.views[i].camera for i in ids]
+        imgs = [small_scene.views[i].image for i in ids]
+        prm, pl, co, sv = _gpu_run(_params(2), cams, imgs)
+        outs[ref] = (pl, co)
+    for ref in range(V):
+        ids = [ref] + [j for j in small_scene.pairs[ref] if j < V][:nsrc]
+        cams = [small_scene.views[i].camera for i in ids]
+        imgs = [small_scene.views[i].image for i in ids]
+        depths = [outs[i][0][..., 3] for i in ids]
+        state = (outs[ref][0], outs[ref][1])
+        p = _params(2)
+        p.geom_consistency = 1
+        prm, pl, co, sv = _gpu_run(p, cams, imgs, depths=depths, state=state)
+        ref_out = oracle.run_patchmatch(prm, cams, imgs, depths=depths, planes=state[0], costs=state[1])
+        assert_bit_exact(pl, ref_out["planes"], f"geom planes view {ref}")
+        assert_bit_exact(co, ref_out["costs"], f"geom costs view {ref}")
+
+
+@pytest.mark.parametrize("W,H", [(37, 33), (40, 65), (9, 7), (64, 31)])
+def test_t3_odd_sizes_and_skipped_row(W, H):
+    """Odd sizes; H=33/65 hit the reference grid's skipped last row."""
+    sc = scene.make_scene(num_views=4, width=W, height=H)
+    cams, imgs = sc.problem(1, 3)
+    prm, pl, co, sv = _gpu_run(_params(2), cams, imgs)
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert_bit_exact(pl, ref["planes"], "planes")
+    assert_bit_exact(co, ref["costs"], "costs")
+    if H in (33, 65):
+        assert oracle.checkerboard_rows(H) == H - 1
+
+
+def test_t3_textureless_gives_nan_costs():
+    """Constant images: every NCC is 2, all sampling probabilities 0, weight
+    norm 0 -> NaN costs (src/ACMMP.cu:1034, :1075, :1091) on both sides."""
+    W, H = 48, 40
+    cams = []
+    K = np.array([[100.0, 0, 24], [0, 100.0, 20], [0, 0, 1]])
+    for i in range(3):
+        R = np.eye(3)
+        t = np.array([-5.0 * i, 0, 0])
+        cams.append(make_camera(K, R, t, W, H, 300, 800))
+    imgs = [np.full((H, W), 77.0, np.float32) for _ in range(3)]
+    prm, pl, co, sv = _gpu_run(_params(2), cams, imgs)
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert np.isnan(ref["costs"]).mean() > 0.5
+    assert_bit_exact(pl, ref["planes"], "planes")
+    assert_bit_exact(co, ref["costs"], "costs")
+
+
+def test_rng_stream_reseeds_second_run(small_scene):
+    """A second RunPatchMatch on the same engine draws a new stream (the
+    reference re-seeds with clock64()); parity holds for both runs."""
+    cams, imgs = small_scene.problem(3, 4)
+    with ACMMP(0) as eng:
+        eng.set_params(_params(1))
+        eng.set_images(cams, imgs)
+        prm0 = eng.params
+        eng.RunPatchMatch()
+        a = eng.plane_hypotheses()
+        prm1 = eng.params
+        eng.RunPatchMatch()
+        b = eng.plane_hypotheses()
+    assert prm1.rng_stream == prm0.rng_stream + 1
+    assert not np.array_equal(a, b)
+    assert_bit_exact(b, oracle.run_patchmatch(prm1, cams, imgs)["planes"], "second run")
