@@ -1285,3 +1285,7 @@ float acmmp_oracle_cosf(float x) { return dm_cosf(x); }
 float acmmp_oracle_acosf(float x) { return dm_acosf(x); }
 
 int acmmp_oracle_checkerboard_rows(int H) { return checkerboard_rows(H); }
+
+uint32_t acmmp_oracle_philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    return dm_philox_x(k0, k1, c0, c1, c2, c3);
+}

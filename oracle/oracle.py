@@ -50,6 +50,8 @@ def _load():
     lib.acmmp_oracle_ncc.argtypes = [P, CAM, CAM, FP, FP, C.c_int, C.c_int, FP]
     lib.acmmp_oracle_homography.restype = None
     lib.acmmp_oracle_homography.argtypes = [CAM, CAM, FP, FP]
+    lib.acmmp_oracle_philox.restype = C.c_uint32
+    lib.acmmp_oracle_philox.argtypes = [C.c_uint32] * 6
     lib.acmmp_oracle_uniform.restype = C.c_float
     lib.acmmp_oracle_uniform.argtypes = [C.c_uint32] * 6
     for name in ("expf", "sinf", "cosf", "acosf"):
@@ -168,6 +170,10 @@ def homography(ref_cam, src_cam, plane):
 
 def uniform(seed_lo, seed_hi, pix, draw, phase, stream):
     return float(_load().acmmp_oracle_uniform(seed_lo, seed_hi, pix, draw, phase, stream))
+
+
+def philox_x(k0, k1, c0, c1, c2, c3):
+    return int(_load().acmmp_oracle_philox(k0, k1, c0, c1, c2, c3))
 
 
 def math_fn(name, x):
