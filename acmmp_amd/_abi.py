@@ -141,6 +141,7 @@ SIGNATURES = {
     "acmmp_eval_geom_costs": (C.c_int, [_CTX, _FP, _FP]),
     "acmmp_set_timing": (C.c_int, [_CTX, C.c_int]),
     "acmmp_get_timing": (C.c_int, [_CTX, C.POINTER(Timing)]),
+    "acmmp_selftest_reciprocal": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "acmmp_device_count": (C.c_int, []),
     "acmmp_version": (C.c_char_p, []),
     "acmmp_read_camera": (C.c_int, [C.c_char_p, C.POINTER(Camera)]),
@@ -160,7 +161,7 @@ def header_symbols(path: str = HEADER) -> list[str]:
 _lib = None
 
 
-def load_library(path: str = LIB_PATH) -> C.CDLL:
+def load_library(path: str | None = None) -> C.CDLL:
     """Load libacmmp_amd.so (built in-tree by __graft_entry__.build()).
 
     Raises a clear error when the native library is missing: there is no
@@ -169,6 +170,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # ACMMP_LIB selects an alternative in-tree build (A/B variants)
+    path = path or os.environ.get("ACMMP_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(
             f"libacmmp_amd.so not found at {path}: build it with "

@@ -766,6 +766,25 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
     return ACMMP_OK;
 }
 
+int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked) {
+    if (!mismatches || !checked) return ACMMP_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    unsigned long long *d = nullptr;
+    if (hipMalloc((void **)&d, 2 * sizeof(unsigned long long)) != hipSuccess) return ACMMP_ERR_HIP;
+    int rc = ACMMP_OK;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        launch_selftest_rcp(d, d + 1, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        rc = ACMMP_ERR_HIP;
+    } else {
+        unsigned long long h[2] = {0, 0};
+        if (hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = ACMMP_ERR_HIP;
+        *mismatches = h[0];
+        *checked = h[1];
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
 int acmmp_set_timing(acmmp_ctx *ctx, int enable) {
     if (!ctx) return ACMMP_ERR_ARG;
     ctx->timing = enable != 0;

@@ -75,6 +75,8 @@ hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float
 hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4 *planes,
                             float *out, hipStream_t stream);
 
+hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);
+
 // Number of checkerboard rows the reference grid reaches (src/ACMMP.cu:1399).
 inline int checkerboard_rows(int H) {
     int gy = ((H / 2) + 16 - 1) / 16;

@@ -32,6 +32,12 @@ namespace acmmp {
 // Patch geometry fixed by the reference defaults (patch_size 11, increment 2:
 // offsets {-5,-3,-1,1,3,5}^2, src/ACMMP.h:34,37). The engine rejects others.
 constexpr int kTaps = 6;
+
+// Minimum waves per SIMD the sweep kernel is register-allocated for
+// (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
+#ifndef ACMMP_SWEEP_WAVES
+#define ACMMP_SWEEP_WAVES 2
+#endif
 constexpr int kSamples = kTaps * kTaps;
 
 // ----------------------------------------------------------------- textures
@@ -223,53 +229,148 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
     H[8] = sc.K[8] * t[8];
 }
 
+// Exactly rounded 1/z. The IEEE division sequence (v_div_scale / v_rcp /
+// 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. ACMMP_FAST_RCP
+// replaces it, inside the exponent window below, by v_rcp_f32 + one fma
+// Newton step — used only if acmmp_selftest_reciprocal() proves the two
+// bit-identical for EVERY float in that window on this hardware.
+#ifndef ACMMP_FAST_RCP
+#define ACMMP_FAST_RCP 1
+#endif
+DEV float recip_newton(float z) {
+    const float r = __builtin_amdgcn_rcpf(z);
+    const float e = dm_fma(-z, r, 1.0f);
+    return dm_fma(e, r, r);
+}
+DEV bool recip_fast_window(float z) {
+    const float az = dm_fabs(z);
+    return az >= 0x1p-125f && az < 0x1p125f;
+}
+DEV float recip_exact(float z) { return 1.0f / z; }
+
+// FAST: v_rcp + Newton (caller guarantees z is inside recip_fast_window).
+template <bool FAST>
+DEV float recip(float z) {
+    if (FAST) return recip_newton(z);
+    return 1.0f / z;
+}
+
 // ComputeCorrespondingPoint (src/ACMMP.cu:324-331), pin P1
 DEV float2 project(const float *H, float x, float y) {
-    const float px = dm_fma(H[0], x, dm_fma(H[1], y, H[2]));
-    const float py = dm_fma(H[3], x, dm_fma(H[4], y, H[5]));
-    const float pz = dm_fma(H[6], x, dm_fma(H[7], y, H[8]));
-    const float inv = 1.0f / pz;
+    const float px = dm_fma(H[1], y, dm_fma(H[0], x, H[2]));
+    const float py = dm_fma(H[4], y, dm_fma(H[3], x, H[5]));
+    const float pz = dm_fma(H[7], y, dm_fma(H[6], x, H[8]));
+    const float inv = recip_exact(pz);
     return make_float2(px * inv, py * inv);
 }
 
-// Invariant reference-side part of ComputeBilateralNCC (src/ACMMP.cu:372-421):
-// everything that does not depend on the source view or the plane.
-struct RefPatch {
+// Source-image sampler: one buffer resource (SRD) per view, built from
+// wave-uniform values (the view index is a uniform loop counter) so the
+// loads are `buffer_load_dwordx2 ... offen` with 32-bit offsets.
+struct SrcImage {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int pitch, W, H;
+};
+
+DEV SrcImage src_image(const KViews &kv, int v) {
+    SrcImage s;
+    s.pitch = kv.ipitch[v];
+    s.W = kv.cam[v].width;
+    s.H = kv.cam[v].height;
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.img[v], (short)0, s.pitch * s.H * 4, 0x00020000);
+    return s;
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// pin P2 (tex2D linear, clamp-to-edge; src/ACMMP.cu:394). The two texels of a
+// row are fetched as one 8-byte load at the clamped column pair
+// xb = clamp(x0, 0, W-2) and selected: for x0 in [-1, W] this reproduces
+// T[clamp(x0)], T[clamp(x0+1)] exactly (engine guarantees W >= 2).
+DEV float bilinear_buf(const SrcImage &im, float u, float v) {
+    float xs = (u + 0.5f) - 0.5f;
+    float ys = (v + 0.5f) - 0.5f;
+    const float fw = (float)im.W, fh = (float)im.H;
+    xs = (xs > -1.0f) ? xs : -1.0f;
+    xs = (xs < fw) ? xs : fw;
+    ys = (ys > -1.0f) ? ys : -1.0f;
+    ys = (ys < fh) ? ys : fh;
+    const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
+    const float ax = xs - fx0, ay = ys - fy0;
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    int xb = x0 < 0 ? 0 : x0;
+    xb = xb > im.W - 2 ? im.W - 2 : xb;
+    const int ya = y0 < 0 ? 0 : (y0 > im.H - 1 ? im.H - 1 : y0);
+    const int yb = (y0 + 1) > (im.H - 1) ? (im.H - 1) : (y0 + 1 < 0 ? 0 : y0 + 1);
+    const u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (ya * im.pitch + xb) * 4, 0, 0);
+    const u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (yb * im.pitch + xb) * 4, 0, 0);
+    const bool lo_right = x0 >= im.W - 1;  // both texels are the last column
+    const bool hi_left = x0 < 0;           // both texels are the first column
+    const float t00 = __uint_as_float(lo_right ? r0.y : r0.x);
+    const float t10 = __uint_as_float(hi_left ? r0.x : r0.y);
+    const float t01 = __uint_as_float(lo_right ? r1.y : r1.x);
+    const float t11 = __uint_as_float(hi_left ? r1.x : r1.y);
+    const float top = dm_fma(ax, t10 - t00, t00);
+    const float bot = dm_fma(ax, t11 - t01, t01);
+    return dm_fma(ay, bot - top, top);
+}
+
+// ---------------------------------------------------------- ref-image tile
+// A block covers 64 colour-split columns (k0..k0+63) x 4 rows (y0..y0+3) of
+// ONE colour c. Both patch offsets i, j are odd, so every reference sample of
+// a colour-c pixel is itself a colour-c pixel: the block's whole reference
+// footprint is a 70 x 14 window of the colour-c plane, staged once in LDS
+// (clamp-to-edge baked in). A wave reads 64 consecutive floats per sample:
+// conflict-free, and the address is a compile-time offset from one base.
+constexpr int kBX = 64, kBY = 4;
+constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
+
+DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
+    const float *img = kv.img[0];
+    const int pitch = kv.ipitch[0], W = kv.W, H = kv.H;
+    for (int e = threadIdx.y * kBX + threadIdx.x; e < kTileW * kTileH; e += kBX * kBY) {
+        const int r = e / kTileW, kk = e - r * kTileW;
+        const int yy = y0 - 5 + r;
+        const int kc = k0 - 3 + kk;
+        const int xx = 2 * kc + ((yy + colour) & 1);
+        tile[e] = texel(img, pitch, W, H, xx, yy);
+    }
+}
+
+// Reference-side invariants of ComputeBilateralNCC (src/ACMMP.cu:372-421):
+// the 36 bilateral weights (ComputeBilateralWeight :353-358) and the
+// normalised ref mean / variance — identical for all 14*(N-1) calls of a
+// pixel-iteration, so computed once (same operations, same order).
+struct PixPatch {
     float w[kSamples];
-    float wr[kSamples];
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
     float inv_wsum;  // inv_bilateral_weight_sum
 };
 
-// ComputeBilateralWeight (src/ACMMP.cu:353-358)
 DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
     const float spatial = dm_sqrt(xd * xd + yd * yd);
     const float color = dm_fabs(pix - cpix);
     return dm_expf(-spatial / (2.0f * ss * ss) - color / (2.0f * sc * sc));
 }
 
-DEV void ref_patch(const KViews &kv, int px, int py, RefPatch &rp) {
-    const float *img = kv.img[0];
-    const int pitch = kv.ipitch[0], W = kv.W, H = kv.H;
+// tb = tile index of sample (ii=0, jj=0) of this lane: ty*kTileW + tx + s
+DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatch &pp) {
     const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
-    const float center = texel(img, pitch, W, H, px, py);
+    const float center = tile[tb - s + 5 * kTileW + 3];
     float sum_ref = 0.0f, sum_rr = 0.0f, bw = 0.0f;
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
-        const int i = -5 + 2 * ii;
         float r_ref = 0.0f, r_rr = 0.0f, r_w = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const int j = -5 + 2 * jj;
-            const float r = texel(img, pitch, W, H, px + i, py + j);
-            const float w = bilateral_weight((float)i, (float)j, r, center, ss, sc);
+            const float r = tile[tb + ii + 2 * kTileW * jj];
+            const float w = bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
             const float wr = w * r;
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
-            rp.w[ii * kTaps + jj] = w;
-            rp.wr[ii * kTaps + jj] = wr;
+            pp.w[ii * kTaps + jj] = w;
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -278,52 +379,138 @@ DEV void ref_patch(const KViews &kv, int px, int py, RefPatch &rp) {
     const float inv = 1.0f / bw;
     sum_ref *= inv;
     sum_rr *= inv;
-    rp.mean = sum_ref;
-    rp.var = sum_rr - sum_ref * sum_ref;
-    rp.inv_wsum = inv;
+    pp.mean = sum_ref;
+    pp.var = sum_rr - sum_ref * sum_ref;
+    pp.inv_wsum = inv;
 }
 
-// ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based).
-DEV float bilateral_ncc(const KViews &kv, const RefPatch &rp, int v, int px, int py, float4 h) {
-    const float cost_max = 2.0f;
-    const float kMinVar = 1e-5f;
-    // var_ref is invariant: when it is below kMinVar (or the centre maps
-    // outside the source) every call returns cost_max.
-    if (rp.var < kMinVar) return cost_max;
-    const acmmp_camera &sc = kv.cam[v];
-    const int sW = sc.width, sH = sc.height;
-    float H[9];
-    homography(kv, v, h, H);
-    const float2 pt = project(H, (float)px, (float)py);
-    if (pt.x >= (float)sW || pt.x < 0.0f || pt.y >= (float)sH || pt.y < 0.0f) return cost_max;
-    const float *img = kv.img[v];
-    const int pitch = kv.ipitch[v];
-    float sum_src = 0.0f, sum_ss = 0.0f, sum_rs = 0.0f;
+// Fetch stage of one patch column (fixed x = px - 5 + 2 ii) of the source
+// samples: projection (pin P1, the x-term hoisted per column), clamp-to-edge
+// addressing (pin P2) and the two 8-byte texel-pair loads per sample.
+struct ColFetch {
+    u32x2 t0[kTaps], t1[kTaps];  // texel pairs of rows clamp(y0), clamp(y0+1)
+    float ax[kTaps], ay[kTaps];   // bilinear weights
+    int x0[kTaps];                // floor column (selects the pair halves)
+};
+
+template <bool FAST>
+DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFetch &f) {
+    const float cx = dm_fma(H[0], x, H[2]);
+    const float cy = dm_fma(H[3], x, H[5]);
+    const float cz = dm_fma(H[6], x, H[8]);
+    const float fw = (float)im.W, fh = (float)im.H;
+#pragma unroll
+    for (int jj = 0; jj < kTaps; ++jj) {
+        const float y = (float)(py - 5 + 2 * jj);
+        const float hx = dm_fma(H[1], y, cx);
+        const float hy = dm_fma(H[4], y, cy);
+        const float hz = dm_fma(H[7], y, cz);
+        const float inv = recip<FAST>(hz);
+        float xs = (hx * inv + 0.5f) - 0.5f;
+        float ys = (hy * inv + 0.5f) - 0.5f;
+        // clamp to [-1, W] x [-1, H]: v_max/v_min (NaN -> -1; bounds are
+        // never +-0, so no signed-zero ambiguity) == the oracle's selects
+        xs = fminf(fmaxf(xs, -1.0f), fw);
+        ys = fminf(fmaxf(ys, -1.0f), fh);
+        const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
+        f.ax[jj] = xs - fx0;
+        f.ay[jj] = ys - fy0;
+        const int x0 = (int)fx0, y0 = (int)fy0;
+        f.x0[jj] = x0;
+        const int xb = min(max(x0, 0), im.W - 2);
+        const int ya = min(max(y0, 0), im.H - 1);
+        const int yb = min(y0 + 1, im.H - 1);  // y0 >= -1
+        f.t0[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (int)(__umul24(ya, im.pitch) + xb) * 4, 0, 0);
+        f.t1[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (int)(__umul24(yb, im.pitch) + xb) * 4, 0, 0);
+    }
+}
+
+// Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
+// software-pipelined one patch column ahead (column ii+1's gathers are in
+// flight while column ii is reduced). Returns the three weighted sums.
+template <bool FAST>
+DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb, const PixPatch &pp, int px,
+                  int py, float &sum_src, float &sum_ss, float &sum_rs) {
+    sum_src = 0.0f;
+    sum_ss = 0.0f;
+    sum_rs = 0.0f;
+    ColFetch buf[2];
+    fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
-        const float x = (float)(px - 5 + 2 * ii);
+        if (ii + 1 < kTaps) fetch_column<FAST>(im, H, (float)(px - 5 + 2 * (ii + 1)), py, buf[(ii + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const ColFetch &f = buf[ii & 1];
         float r_s = 0.0f, r_ss = 0.0f, r_rs = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const float y = (float)(py - 5 + 2 * jj);
-            const float2 q = project(H, x, y);
-            const float s = bilinear(img, pitch, sW, sH, q.x, q.y);
-            const float ws = rp.w[ii * kTaps + jj] * s;
+            const bool lo_right = f.x0[jj] >= im.W - 1;  // both texels are the last column
+            const bool hi_left = f.x0[jj] < 0;           // both texels are the first column
+            const float t00 = __uint_as_float(lo_right ? f.t0[jj].y : f.t0[jj].x);
+            const float t10 = __uint_as_float(hi_left ? f.t0[jj].x : f.t0[jj].y);
+            const float t01 = __uint_as_float(lo_right ? f.t1[jj].y : f.t1[jj].x);
+            const float t11 = __uint_as_float(hi_left ? f.t1[jj].x : f.t1[jj].y);
+            const float top = dm_fma(f.ax[jj], t10 - t00, t00);
+            const float bot = dm_fma(f.ax[jj], t11 - t01, t01);
+            const float sv = dm_fma(f.ay[jj], bot - top, top);
+            const float w = pp.w[ii * kTaps + jj];
+            const float wr = w * tile[tb + ii + 2 * kTileW * jj];
+            const float ws = w * sv;
             r_s += ws;
-            r_ss = dm_fma(ws, s, r_ss);
-            r_rs = dm_fma(rp.wr[ii * kTaps + jj], s, r_rs);
+            r_ss = dm_fma(ws, sv, r_ss);
+            r_rs = dm_fma(wr, sv, r_rs);
         }
         sum_src += r_s;
         sum_ss += r_ss;
         sum_rs += r_rs;
+        __builtin_amdgcn_sched_barrier(0);
     }
-    sum_src *= rp.inv_wsum;
-    sum_ss *= rp.inv_wsum;
-    sum_rs *= rp.inv_wsum;
+}
+
+// ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
+// wave-uniform). Reference samples come from the LDS tile, source samples
+// through ncc_sums.
+DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
+                        int py, float4 h) {
+    const float cost_max = 2.0f;
+    const float kMinVar = 1e-5f;
+    // var_ref is invariant: when it is below kMinVar (or the centre maps
+    // outside the source) every call returns cost_max.
+    if (pp.var < kMinVar) return cost_max;
+    const SrcImage im = src_image(kv, v);
+    float H[9];
+    homography(kv, v, h, H);
+    const float2 pt = project(H, (float)px, (float)py);
+    if (pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f) return cost_max;
+    // re-read the reference samples from LDS (cheap, conflict-free) instead
+    // of letting the compiler keep all 36 in VGPRs across calls
+    asm volatile("" : "+v"(tb));
+    float sum_src, sum_ss, sum_rs;
+#if ACMMP_FAST_RCP
+    // hz is affine in the sample position, so its values over the patch lie
+    // between the four corner values (up to rounding: the window test uses a
+    // 2x margin). Inside the window the Newton reciprocal is bit-identical to
+    // IEEE 1/z (exhaustive proof: acmmp_selftest_reciprocal).
+    const float xl = (float)(px - 5), xr = (float)(px + 5), yt = (float)(py - 5), yb = (float)(py + 5);
+    const float z00 = dm_fma(H[7], yt, dm_fma(H[6], xl, H[8]));
+    const float z10 = dm_fma(H[7], yt, dm_fma(H[6], xr, H[8]));
+    const float z01 = dm_fma(H[7], yb, dm_fma(H[6], xl, H[8]));
+    const float z11 = dm_fma(H[7], yb, dm_fma(H[6], xr, H[8]));
+    const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
+    const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
+    const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
+    if (fast) ncc_sums<true>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
+    else ncc_sums<false>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
+#else
+    ncc_sums<false>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
+#endif
+    sum_src *= pp.inv_wsum;
+    sum_ss *= pp.inv_wsum;
+    sum_rs *= pp.inv_wsum;
     const float var_src = sum_ss - sum_src * sum_src;
     if (var_src < kMinVar) return cost_max;
-    const float covar = sum_rs - rp.mean * sum_src;
-    const float var_rs = dm_sqrt(rp.var * var_src);
+    const float covar = sum_rs - pp.mean * sum_src;
+    const float var_rs = dm_sqrt(pp.var * var_src);
     float c = 1.0f - covar / var_rs;
     c = (c < cost_max) ? c : cost_max;
     c = (c > 0.0f) ? c : 0.0f;
@@ -332,19 +519,19 @@ DEV float bilateral_ncc(const KViews &kv, const RefPatch &rp, int v, int px, int
 
 // ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
 template <int NS>
-DEV float initial_cost(const KViews &kv, const RefPatch &rp, int px, int py, float4 h, uint32_t &sel) {
+DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int px, int py,
+                       float4 h, uint32_t &sel) {
     const int nsrc = kv.nsrc;
     float cv[NS];
     float cs[NS];
     int num_valid = 0;
     for (int i = 0; i < nsrc; ++i) {
-        const float c = bilateral_ncc(kv, rp, i + 1, px, py, h);
+        const float c = bilateral_ncc(kv, tile, tb, pp, i + 1, px, py, h);
         cv[i] = c;
         cs[i] = c;
         if (c < 2.0f) num_valid++;
     }
-    // sort_small (src/ACMMP.cu:24-33)
-    for (int i = 1; i < nsrc; i++) {
+    for (int i = 1; i < nsrc; i++) {  // sort_small (src/ACMMP.cu:24-33)
         const float tmp = cs[i];
         int j;
         for (j = i; j >= 1 && tmp < cs[j - 1]; j--) cs[j] = cs[j - 1];
@@ -363,7 +550,6 @@ DEV float initial_cost(const KViews &kv, const RefPatch &rp, int px, int py, flo
     return 2.0f;
 }
 
-// ComputeGeomConsistencyCost (src/ACMMP.cu:518-543)
 DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
     const float max_cost = 3.0f;
     const acmmp_camera &rc = kv.cam[0];
@@ -470,21 +656,67 @@ DEV float4 upscale_normal(const KViews &kv, const KState &st, int px, int py, fl
     return n_total;
 }
 
+// ------------------------------------------------------ colour-split lanes
+// Every PatchMatch kernel maps a 64x4 block onto 64 colour-split columns x 4
+// rows of ONE checkerboard colour: lane (tx, ty) of block (bx, by) handles
+// pixel x = 2k + s, y, with k = 64 bx + tx, y = 4 by + ty, s = (y + colour) & 1.
+struct LaneGeom {
+    int k, px, py, s, tb;
+};
+
+// XCD-aware block order (cdna_hip_programming.md T1): workgroups are dealt
+// round-robin to the 8 XCDs, so consecutive (x, y) blocks would land on 8
+// different L2s. Remap the dispatch index so XCD j processes one contiguous
+// run of blocks (a band of rows): its L2 then holds the source-image
+// footprint of that band only. Bijective for any block count; affects speed
+// only (dispatch placement is not guaranteed).
+struct BlockXY {
+    int bx, by;
+};
+
+DEV BlockXY xcd_block() {
+    const int gx = gridDim.x;
+    const int T = gx * gridDim.y;
+    const int L = blockIdx.y * gx + blockIdx.x;
+    const int xcd = L & 7, i = L >> 3;
+    const int q = T >> 3, r = T & 7;
+    const int nl = (xcd < r) ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+    BlockXY b;
+    b.by = nl / gx;
+    b.bx = nl - b.by * gx;
+    return b;
+}
+
+DEV LaneGeom lane_geom(int colour, BlockXY b) {
+    LaneGeom g;
+    g.k = b.bx * kBX + threadIdx.x;
+    g.py = b.by * kBY + threadIdx.y;
+    g.s = (g.py + colour) & 1;
+    g.px = 2 * g.k + g.s;
+    g.tb = threadIdx.y * kTileW + threadIdx.x + g.s;
+    return g;
+}
+
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
-// writes the colour-split "current" buffers.
+// writes the colour-split "current" buffers. blockIdx.z = colour.
 template <int NS>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
+    __shared__ float tile[kTileW * kTileH];
     const KViews &kv = *kvp;
-    const int px = blockIdx.x * 64 + threadIdx.x;
-    const int py = blockIdx.y * 4 + threadIdx.y;
+    const int colour = blockIdx.z;
+    const BlockXY blk = xcd_block();
+    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    __syncthreads();
+    const LaneGeom g = lane_geom(colour, blk);
+    const int px = g.px, py = g.py;
     if (px >= kv.W || py >= kv.H) return;
     const acmmp_params &prm = kv.prm;
     const acmmp_camera &c0 = kv.cam[0];
     const int center = py * kv.W + px;
     dm_rng rs = make_rng(kv, center, 0u);
-    RefPatch rp;
-    ref_patch(kv, px, py, rp);
+    PixPatch pp;
+    pixel_patch(kv, tile, g.tb, g.s, pp);
     float4 plane;
     float cost;
     uint32_t sel = 0;
@@ -492,10 +724,10 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         const float depth = dm_rng_uniform(&rs) * (prm.depth_max - prm.depth_min) + prm.depth_min;
         plane = random_normal(c0, px, py, rs, depth);
         plane.w = distance_to_origin(c0, px, py, depth, plane);
-        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.seeded) {
         plane = st.seed[center];
-        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.planar_prior) {
         if (st.mask[center] > 0 && st.rm_cost[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -510,7 +742,7 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
             plane = st.rm_plane[center];
             plane.w = distance_to_origin(c0, px, py, plane.w, plane);
         }
-        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.upsample) {
         const float scale = (float)(1.0 * (double)prm.scaled_cols / (double)kv.W);
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -522,42 +754,54 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         float ucost;
         const float4 n_total = upscale_normal(kv, st, px, py, sigmad, sigmar, nn, o_y, o_x, refPix, ucost);
         const float4 prev = st.rm_plane[center];
-        const float c_pre = initial_cost<NS>(kv, rp, px, py, prev, sel);
-        st.pre_cost[center] = c_pre;
+        st.pre_cost[center] = initial_cost<NS>(kv, tile, g.tb, pp, px, py, prev, sel);
         plane = to_cam(c0, n_total);
         plane.w = distance_to_origin(c0, px, py, prev.w, plane);
-        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else {
         float4 h = prm.hierarchy ? st.scaled[center] : st.rm_plane[center];
         h = to_cam(c0, h);
         h.w = distance_to_origin(c0, px, py, h.w, h);
         plane = h;
-        cost = initial_cost<NS>(kv, rp, px, py, plane, sel);
+        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
     }
-    const int c = (px + py) & 1;
-    const int ci = cs_index(kv, px, py);
-    st.plane[c][ci] = plane;
-    st.cost[c][ci] = cost;
-    st.sv[c][ci] = sel;
+    const int ci = py * kv.Wh + g.k;
+    st.plane[colour][ci] = plane;
+    st.cost[colour][ci] = cost;
+    st.sv[colour][ci] = sel;
 }
+
+// Packed per-view sample counts (view_weights of the reference, src/ACMMP.cu:995):
+// 15 draws, so every count fits 4 bits; 32 views -> two 64-bit words.
+struct ViewCounts {
+    uint64_t lo = 0, hi = 0;
+    __device__ __forceinline__ void add(int j) {
+        if (j < 16) lo += (uint64_t)1 << (4 * j);
+        else hi += (uint64_t)1 << (4 * (j - 16));
+    }
+    __device__ __forceinline__ int get(int j) const { return (int)(((j < 16) ? (lo >> (4 * j)) : (hi >> (4 * (j - 16)))) & 15u); }
+};
 
 // ------------------------------------------------------------- the sweep
 // CheckerboardPropagation (src/ACMMP.cu:786-1173) for the pixels of one colour.
-// Lane (k, y) -> pixel x = 2k + ((y + colour) & 1). Neighbour state is read
-// from the colour-split "current" buffers (the half-sweep snapshot); own state
-// is kept in registers and written to the "next" buffer of this colour.
+// Neighbour state is read from the colour-split "current" buffers (the
+// half-sweep snapshot); own state lives in registers and is written to the
+// "next" buffer of this colour.
 template <int NS>
-__global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
-                                               int iter) {
+__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
+                                                  int iter) {
+    __shared__ float tile[kTileW * kTileH];
     const KViews &kv = *kvp;
-    const int k = blockIdx.x * 64 + threadIdx.x;
-    const int py = blockIdx.y * 4 + threadIdx.y;
+    const BlockXY blk = xcd_block();
+    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    __syncthreads();
+    const LaneGeom g = lane_geom(colour, blk);
+    const int px = g.px, py = g.py;
     const int width = kv.W, height = kv.H;
-    if (py >= height) return;
-    const int px = 2 * k + ((py + colour) & 1);
-    if (px >= width) return;
+    if (py >= height || px >= width) return;
     const int oc = colour ^ 1;
-    const int my = cs_index(kv, px, py);
+    const int Wh = kv.Wh;
+    const int my = py * Wh + g.k;
     const float4 *plane_same = st.plane[colour];
     const float4 *plane_opp = st.plane[oc];
     const float *cost_same = st.cost[colour];
@@ -574,191 +818,193 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
     const acmmp_camera &c0 = kv.cam[0];
     const int nsrc = kv.nsrc;
     const int center = py * width + px;
+#define CS(x, y) ((y) * Wh + ((x) >> 1))
 
-    // ---- adaptive checkerboard sampling (:813-991); positions kept as (x, y)
-    int posx[8], posy[8];
-    bool flag[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) { flag[d] = false; posx[d] = px; posy[d] = py; }
+    // ---- adaptive checkerboard sampling (:813-991). cidx[d]: colour-split
+    // index of direction d's winner; bit d of `same`: it is this colour.
+    int cidx[8];
+    uint32_t flags = 0, same = 0;
     float costMin;
-    // up_far (opposite colour)
-    if (py > 2) {
-        flag[1] = true;
+    if (py > 2) {  // up_far (opposite colour)
+        flags |= 1u << 1;
         int by = py - 3;
-        costMin = cost_opp[cs_index(kv, px, by)];
+        costMin = cost_opp[CS(px, by)];
         for (int i = 1; i < 11; ++i) {
             if (py > 2 + 2 * i) {
                 const int ty = py - 3 - 2 * i;
-                const float c = cost_opp[cs_index(kv, px, ty)];
+                const float c = cost_opp[CS(px, ty)];
                 if (c < costMin) { costMin = c; by = ty; }
             }
         }
-        posy[1] = by;
+        cidx[1] = CS(px, by);
     }
     if (py < height - 3) {  // down_far
-        flag[3] = true;
+        flags |= 1u << 3;
         int by = py + 3;
-        costMin = cost_opp[cs_index(kv, px, by)];
+        costMin = cost_opp[CS(px, by)];
         for (int i = 1; i < 11; ++i) {
             if (py < height - 3 - 2 * i) {
                 const int ty = py + 3 + 2 * i;
-                const float c = cost_opp[cs_index(kv, px, ty)];
+                const float c = cost_opp[CS(px, ty)];
                 if (c < costMin) { costMin = c; by = ty; }
             }
         }
-        posy[3] = by;
+        cidx[3] = CS(px, by);
     }
     if (px > 2) {  // left_far
-        flag[5] = true;
+        flags |= 1u << 5;
         int bx = px - 3;
-        costMin = cost_opp[cs_index(kv, bx, py)];
+        costMin = cost_opp[CS(bx, py)];
         for (int i = 1; i < 11; ++i) {
             if (px > 2 + 2 * i) {
                 const int tx = px - 3 - 2 * i;
-                const float c = cost_opp[cs_index(kv, tx, py)];
+                const float c = cost_opp[CS(tx, py)];
                 if (c < costMin) { costMin = c; bx = tx; }
             }
         }
-        posx[5] = bx;
+        cidx[5] = CS(bx, py);
     }
     if (px < width - 3) {  // right_far: reversed comparison keeps the max (:879)
-        flag[7] = true;
+        flags |= 1u << 7;
         int bx = px + 3;
-        costMin = cost_opp[cs_index(kv, bx, py)];
+        costMin = cost_opp[CS(bx, py)];
         for (int i = 1; i < 11; ++i) {
             if (px < width - 3 - 2 * i) {
                 const int tx = px + 3 + 2 * i;
-                const float c = cost_opp[cs_index(kv, tx, py)];
+                const float c = cost_opp[CS(tx, py)];
                 if (costMin < c) { costMin = c; bx = tx; }
             }
         }
-        posx[7] = bx;
+        cidx[7] = CS(bx, py);
     }
-    // near "V" searches: base point is the opposite colour, the V arms are
-    // the same colour (read from the snapshot).
+    // near "V" searches: the base point is the opposite colour, the V arms
+    // are this colour (snapshot reads, pin A2).
     if (py > 0) {  // up_near
-        flag[0] = true;
-        int bx = px, by = py - 1;
-        costMin = cost_opp[cs_index(kv, bx, by)];
+        flags |= 1u << 0;
+        int bi = CS(px, py - 1);
+        bool bs = false;
+        costMin = cost_opp[bi];
         for (int i = 0; i < 3; ++i) {
             const int ty = py - 2 - i;
             if (py > 1 + i && px > i) {
-                const float c = cost_same[cs_index(kv, px - i, ty)];
-                if (c < costMin) { costMin = c; bx = px - i; by = ty; }
+                const float c = cost_same[CS(px - i, ty)];
+                if (c < costMin) { costMin = c; bi = CS(px - i, ty); bs = true; }
             }
             if (py > 1 + i && px < width - 1 - i) {
-                const float c = cost_same[cs_index(kv, px + i, ty)];
-                if (c < costMin) { costMin = c; bx = px + i; by = ty; }
+                const float c = cost_same[CS(px + i, ty)];
+                if (c < costMin) { costMin = c; bi = CS(px + i, ty); bs = true; }
             }
         }
-        posx[0] = bx; posy[0] = by;
+        cidx[0] = bi;
+        same |= (uint32_t)bs << 0;
     }
     if (py < height - 1) {  // down_near
-        flag[2] = true;
-        int bx = px, by = py + 1;
-        costMin = cost_opp[cs_index(kv, bx, by)];
+        flags |= 1u << 2;
+        int bi = CS(px, py + 1);
+        bool bs = false;
+        costMin = cost_opp[bi];
         for (int i = 0; i < 3; ++i) {
             const int ty = py + 2 + i;
             if (py < height - 2 - i && px > i) {
-                const float c = cost_same[cs_index(kv, px - i, ty)];
-                if (c < costMin) { costMin = c; bx = px - i; by = ty; }
+                const float c = cost_same[CS(px - i, ty)];
+                if (c < costMin) { costMin = c; bi = CS(px - i, ty); bs = true; }
             }
             if (py < height - 2 - i && px < width - 1 - i) {
-                const float c = cost_same[cs_index(kv, px + i, ty)];
-                if (c < costMin) { costMin = c; bx = px + i; by = ty; }
+                const float c = cost_same[CS(px + i, ty)];
+                if (c < costMin) { costMin = c; bi = CS(px + i, ty); bs = true; }
             }
         }
-        posx[2] = bx; posy[2] = by;
+        cidx[2] = bi;
+        same |= (uint32_t)bs << 2;
     }
     if (px > 0) {  // left_near
-        flag[4] = true;
-        int bx = px - 1, by = py;
-        costMin = cost_opp[cs_index(kv, bx, by)];
+        flags |= 1u << 4;
+        int bi = CS(px - 1, py);
+        bool bs = false;
+        costMin = cost_opp[bi];
         for (int i = 0; i < 3; ++i) {
             const int tx = px - 2 - i;
             if (px > 1 + i && py > i) {
-                const float c = cost_same[cs_index(kv, tx, py - i)];
-                if (c < costMin) { costMin = c; bx = tx; by = py - i; }
+                const float c = cost_same[CS(tx, py - i)];
+                if (c < costMin) { costMin = c; bi = CS(tx, py - i); bs = true; }
             }
             if (px > 1 + i && py < height - 1 - i) {
-                const float c = cost_same[cs_index(kv, tx, py + i)];
-                if (c < costMin) { costMin = c; bx = tx; by = py + i; }
+                const float c = cost_same[CS(tx, py + i)];
+                if (c < costMin) { costMin = c; bi = CS(tx, py + i); bs = true; }
             }
         }
-        posx[4] = bx; posy[4] = by;
+        cidx[4] = bi;
+        same |= (uint32_t)bs << 4;
     }
     if (px < width - 1) {  // right_near
-        flag[6] = true;
-        int bx = px + 1, by = py;
-        costMin = cost_opp[cs_index(kv, bx, by)];
+        flags |= 1u << 6;
+        int bi = CS(px + 1, py);
+        bool bs = false;
+        costMin = cost_opp[bi];
         for (int i = 0; i < 3; ++i) {
             const int tx = px + 2 + i;
             if (px < width - 2 - i && py > i) {
-                const float c = cost_same[cs_index(kv, tx, py - i)];
-                if (c < costMin) { costMin = c; bx = tx; by = py - i; }
+                const float c = cost_same[CS(tx, py - i)];
+                if (c < costMin) { costMin = c; bi = CS(tx, py - i); bs = true; }
             }
             if (px < width - 2 - i && py < height - 1 - i) {
-                const float c = cost_same[cs_index(kv, tx, py + i)];
-                if (c < costMin) { costMin = c; bx = tx; by = py + i; }
+                const float c = cost_same[CS(tx, py + i)];
+                if (c < costMin) { costMin = c; bi = CS(tx, py + i); bs = true; }
             }
         }
-        posx[6] = bx; posy[6] = by;
+        cidx[6] = bi;
+        same |= (uint32_t)bs << 6;
     }
-    float4 cand[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-        const int qx = posx[d], qy = posy[d];
-        const float4 *src = (((qx + qy) & 1) == colour) ? plane_same : plane_opp;
-        cand[d] = flag[d] ? src[cs_index(kv, qx, qy)] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+#undef CS
+    auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
 
-    RefPatch rp;
-    ref_patch(kv, px, py, rp);
+    PixPatch pp;
+    pixel_patch(kv, tile, g.tb, g.s, pp);
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
     for (int d = 0; d < 8; ++d) {
-        if (flag[d]) {
-            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = bilateral_ncc(kv, rp, v + 1, px, py, cand[d]);
+        if ((flags >> d) & 1u) {
+            const float4 h = cand(d);
+            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, h);
         } else {
             for (int v = 0; v < nsrc; ++v) cost_array[d][v] = (d == 0 && v == 0) ? 2.0f : 0.0f;
         }
     }
 
     // ---- multi-hypothesis joint view selection (:994-1056)
-    float vsp[NS];
-    for (int j = 0; j < nsrc; ++j) vsp[j] = 0.0f;
+    float probs[NS];
     {
         const uint32_t *sv_opp = st.sv[oc];
+        const int kc = g.k;
         uint32_t nb[4];
-        nb[0] = (py > 0) ? sv_opp[cs_index(kv, px, py - 1)] : 0u;
-        nb[1] = (py < height - 1) ? sv_opp[cs_index(kv, px, py + 1)] : 0u;
-        nb[2] = (px > 0) ? sv_opp[cs_index(kv, px - 1, py)] : 0u;
-        nb[3] = (px < width - 1) ? sv_opp[cs_index(kv, px + 1, py)] : 0u;
-        for (int i = 0; i < 4; ++i) {
-            if (flag[2 * i]) {
-                for (int j = 0; j < nsrc; ++j) vsp[j] += ((nb[i] >> j) & 1u) ? 0.9f : 0.1f;
+        // (x, y+-1) are colour-split column (x >> 1); (x+-1, y) are k - 1 + s, k + s
+        nb[0] = (py > 0) ? sv_opp[(py - 1) * Wh + (px >> 1)] : 0u;
+        nb[1] = (py < height - 1) ? sv_opp[(py + 1) * Wh + (px >> 1)] : 0u;
+        nb[2] = (px > 0) ? sv_opp[py * Wh + ((px - 1) >> 1)] : 0u;
+        nb[3] = (px < width - 1) ? sv_opp[py * Wh + ((px + 1) >> 1)] : 0u;
+        (void)kc;
+        const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
+        for (int i = 0; i < nsrc; i++) {
+            float vsp = 0.0f;
+            for (int n = 0; n < 4; ++n)
+                if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> i) & 1u) ? 0.9f : 0.1f;
+            float count = 0;
+            int count_false = 0;
+            float tmpw = 0;
+            for (int j = 0; j < 8; j++) {
+                const float c = cost_array[j][i];
+                if (c < cost_threshold) {
+                    tmpw += dm_expf(c * c / (-0.18f));
+                    count++;
+                }
+                if (c > 1.2f) count_false++;
             }
+            float pr = 0.0f;
+            if (count > 2 && count_false < 3) pr = tmpw / count;
+            else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
+            probs[i] = pr * vsp;
         }
-    }
-    float probs[NS];
-    const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
-    for (int i = 0; i < nsrc; i++) {
-        float count = 0;
-        int count_false = 0;
-        float tmpw = 0;
-        for (int j = 0; j < 8; j++) {
-            const float c = cost_array[j][i];
-            if (c < cost_threshold) {
-                tmpw += dm_expf(c * c / (-0.18f));
-                count++;
-            }
-            if (c > 1.2f) count_false++;
-        }
-        float pr = 0.0f;
-        if (count > 2 && count_false < 3) pr = tmpw / count;
-        else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
-        probs[i] = pr * vsp[i];
     }
     {  // TransformPDFToCDF (:107-121)
         float sum = 0.0f;
@@ -771,30 +1017,34 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
         }
     }
     dm_rng rs = make_rng(kv, center, 1u + (uint32_t)iter);
-    float view_weights[NS];
-    for (int j = 0; j < nsrc; ++j) view_weights[j] = 0.0f;
+    ViewCounts vw;
     for (int sample = 0; sample < 15; ++sample) {
         const float rand_prob = dm_rng_uniform(&rs) - FLT_EPSILON;
         for (int image_id = 0; image_id < nsrc; ++image_id) {
-            if (probs[image_id] > rand_prob) { view_weights[image_id] += 1.0f; break; }
+            if (probs[image_id] > rand_prob) { vw.add(image_id); break; }
         }
     }
     uint32_t temp_sv = 0;
     float weight_norm = 0;
     for (int i = 0; i < nsrc; ++i) {
-        if (view_weights[i] > 0) { temp_sv |= (1u << i); weight_norm += view_weights[i]; }
+        const int c = vw.get(i);
+        if (c > 0) { temp_sv |= (1u << i); weight_norm += (float)c; }
     }
 
     float final_costs[8];
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
+        const bool fl = (flags >> i) & 1u;
+        float4 hi = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (prm.geom_consistency && fl) hi = cand(i);
         for (int j = 0; j < nsrc; ++j) {
-            if (view_weights[j] > 0) {
+            const float wj = (float)vw.get(j);
+            if (wj > 0) {
                 if (prm.geom_consistency) {
-                    if (flag[i]) fc += view_weights[j] * (cost_array[i][j] + 0.2f * geom_cost(kv, j + 1, cand[i], px, py));
-                    else fc += view_weights[j] * (cost_array[i][j] + 0.1f * 3.0f);
+                    if (fl) fc += wj * (cost_array[i][j] + 0.2f * geom_cost(kv, j + 1, hi, px, py));
+                    else fc += wj * (cost_array[i][j] + 0.1f * 3.0f);
                 } else {
-                    fc += view_weights[j] * cost_array[i][j];
+                    fc += wj * cost_array[i][j];
                 }
             }
         }
@@ -830,12 +1080,15 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
             h = ref_normals[t - 1];
             h.w = distance_to_origin(c0, px, py, ref_depths[t - 1], h);
         }
+        // views with a zero sampled weight contribute +0 in the reference
+        // (weight 0 * finite cost), so their NCC is skipped: bit-identical
         float tc = 0.0f;
         for (int j = 0; j < nsrc; ++j) {
-            if (view_weights[j] > 0) {
-                const float c = bilateral_ncc(kv, rp, j + 1, px, py, h);
-                if (prm.geom_consistency) tc += view_weights[j] * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
-                else tc += view_weights[j] * c;
+            const float wj = (float)vw.get(j);
+            if (wj > 0) {
+                const float c = bilateral_ncc(kv, tile, g.tb, pp, j + 1, px, py, h);
+                if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
+                else tc += wj * c;
             }
         }
         tc /= weight_norm;
@@ -849,10 +1102,11 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
                     float rfc[8];
                     for (int i = 0; i < 8; i++) {
                         rfc[i] = 0.0f;
-                        if (flag[i]) {
-                            const float dn = plane_depth(c0, cand[i], px, py);
+                        if ((flags >> i) & 1u) {
+                            const float4 ci = cand(i);
+                            const float dn = plane_depth(c0, ci, px, py);
                             const float dd = dn - depth_prior;
-                            const float ad = dm_acosf(dot3(prior_plane, cand[i]));
+                            const float ad = dm_acosf(dot3(prior_plane, ci));
                             const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
                             rfc[i] = dm_expf(-final_costs[i] * final_costs[i] / beta) * prior;
                         }
@@ -868,32 +1122,35 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
                     const float ad = dm_acosf(dot3(prior_plane, my_plane));
                     const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
                     const float rcn = dm_expf(-cost_now * cost_now / beta) * prior;
-                    if (flag[max_idx]) {
-                        const float db = plane_depth(c0, cand[max_idx], px, py);
+                    if ((flags >> max_idx) & 1u) {
+                        const float4 cm = cand(max_idx);
+                        const float db = plane_depth(c0, cm, px, py);
                         if (db >= prm.depth_min && db <= prm.depth_max && rfc[max_idx] > rcn) {
                             // the reference assigns a shadowing local here (:1119/:1130):
                             // the outer depth_now is NOT updated
-                            my_plane = cand[max_idx];
+                            my_plane = cm;
                             my_cost = final_costs[max_idx];
                             restricted_cost = rfc[max_idx];
                             my_sv = temp_sv;
                         }
                     }
-                } else if (flag[min_cost_idx]) {
-                    const float db = plane_depth(c0, cand[min_cost_idx], px, py);
+                } else if ((flags >> min_cost_idx) & 1u) {
+                    const float4 cm = cand(min_cost_idx);
+                    const float db = plane_depth(c0, cm, px, py);
                     if (db >= prm.depth_min && db <= prm.depth_max && final_costs[min_cost_idx] < cost_now) {
                         depth_now = db;
-                        my_plane = cand[min_cost_idx];
+                        my_plane = cm;
                         my_cost = final_costs[min_cost_idx];
                     }
                 }
             }
             plane_now = my_plane;  // pin A3
-            if (!prm.planar_prior && flag[min_cost_idx]) {
-                const float db = plane_depth(c0, cand[min_cost_idx], px, py);
+            if (!prm.planar_prior && ((flags >> min_cost_idx) & 1u)) {
+                const float4 cm = cand(min_cost_idx);
+                const float db = plane_depth(c0, cm, px, py);
                 if (db >= prm.depth_min && db <= prm.depth_max && final_costs[min_cost_idx] < cost_now) {
                     depth_now = db;
-                    plane_now = cand[min_cost_idx];
+                    plane_now = cm;
                     cost_now = final_costs[min_cost_idx];
                     my_sv = temp_sv;
                 }
@@ -960,8 +1217,6 @@ __global__ __launch_bounds__(256) void k_sweep(const KViews *__restrict__ kvp, K
     st.sv[colour][my] = my_sv;
 }
 
-// GetDepthandNormal (src/ACMMP.cu:1199-1212) fused with the colour-split ->
-// row-major conversion.
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
     const KViews &kv = *kvp;
     const int px = blockIdx.x * 64 + threadIdx.x;
@@ -1029,22 +1284,29 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
 }
 
 // T1 kernel: costs of a given plane per pixel against every source view.
+// T1 kernel: costs of a given plane per pixel against every source view
+// (same NCC code path as the sweep; blockIdx.z = colour).
 template <int NS>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
+    __shared__ float tile[kTileW * kTileH];
     const KViews &kv = *kvp;
-    const int px = blockIdx.x * 64 + threadIdx.x;
-    const int py = blockIdx.y * 4 + threadIdx.y;
-    if (px >= kv.W || py >= kv.H) return;
-    const int c = py * kv.W + px;
-    RefPatch rp;
-    ref_patch(kv, px, py, rp);
+    const int colour = blockIdx.z;
+    const BlockXY blk = xcd_block();
+    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    __syncthreads();
+    const LaneGeom g = lane_geom(colour, blk);
+    if (g.px >= kv.W || g.py >= kv.H) return;
+    const int c = g.py * kv.W + g.px;
+    PixPatch pp;
+    pixel_patch(kv, tile, g.tb, g.s, pp);
     const float4 h = planes[c];
     if (out)
-        for (int v = 0; v < kv.nsrc; ++v) out[(size_t)c * kv.nsrc + v] = bilateral_ncc(kv, rp, v + 1, px, py, h);
+        for (int v = 0; v < kv.nsrc; ++v)
+            out[(size_t)c * kv.nsrc + v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
     if (out_init) {
         uint32_t sel = 0;
-        out_init[c] = initial_cost<NS>(kv, rp, px, py, h, sel);
+        out_init[c] = initial_cost<NS>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
         if (out_views) out_views[c] = sel;
     }
 }
@@ -1059,6 +1321,30 @@ __global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kv
     for (int v = 0; v < kv.nsrc; ++v) out[(size_t)c * kv.nsrc + v] = geom_cost(kv, v + 1, planes[c], px, py);
 }
 
+// Exhaustive check of recip_newton against IEEE 1/z over every float32 bit
+// pattern inside recip_fast_window (grid-stride over all 2^32 patterns).
+__global__ __launch_bounds__(256) void k_selftest_rcp(unsigned long long *mismatch,
+                                                      unsigned long long *checked) {
+    unsigned long long bad = 0, n = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < (1ull << 32); u += stride) {
+        const float z = __uint_as_float((uint32_t)u);
+        if (!recip_fast_window(z)) continue;
+        ++n;
+        const float a = recip_newton(z);
+        volatile float one = 1.0f;
+        const float b = one / z;
+        if (__float_as_uint(a) != __float_as_uint(b)) ++bad;
+    }
+    atomicAdd(mismatch, bad);
+    atomicAdd(checked, n);
+}
+
+hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s) {
+    k_selftest_rcp<<<4096, 256, 0, s>>>(mismatch, checked);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 // Source-view count -> array capacity of the templated kernels.
 static int ns_bucket(int nsrc) {
@@ -1069,37 +1355,27 @@ static int ns_bucket(int nsrc) {
     return 32;
 }
 
-#define ACMMP_DISPATCH_NS(nsrc, KERNEL, ...)                  \
-    switch (ns_bucket(nsrc)) {                                \
-        case 4: KERNEL<4><<<__VA_ARGS__>>>; break;            \
-        case 9: KERNEL<9><<<__VA_ARGS__>>>; break;            \
-        case 16: KERNEL<16><<<__VA_ARGS__>>>; break;          \
-        case 20: KERNEL<20><<<__VA_ARGS__>>>; break;          \
-        default: KERNEL<32><<<__VA_ARGS__>>>; break;          \
+#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
+    switch (ns_bucket(h_kv.nsrc)) {                                                         \
+        case 4: KERNEL<4><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                  \
+        case 9: KERNEL<9><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                  \
+        case 16: KERNEL<16><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
+        case 20: KERNEL<20><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
+        default: KERNEL<32><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
     }
 
+static dim3 cs_grid(const KViews &kv, int colours) {
+    return dim3((kv.Wh + kBX - 1) / kBX, (kv.H + kBY - 1) / kBY, colours);
+}
+
 hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
-    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
-    switch (ns_bucket(h_kv.nsrc)) {
-        case 4: k_init<4><<<grid, block, 0, stream>>>(d_kv, st); break;
-        case 9: k_init<9><<<grid, block, 0, stream>>>(d_kv, st); break;
-        case 16: k_init<16><<<grid, block, 0, stream>>>(d_kv, st); break;
-        case 20: k_init<20><<<grid, block, 0, stream>>>(d_kv, st); break;
-        default: k_init<32><<<grid, block, 0, stream>>>(d_kv, st); break;
-    }
+    ACMMP_LAUNCH_NS(k_init, cs_grid(h_kv, 2), dim3(kBX, kBY), stream, d_kv, st);
     return hipGetLastError();
 }
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
-    dim3 block(64, 4), grid((h_kv.Wh + 63) / 64, (h_kv.H + 3) / 4);
-    switch (ns_bucket(h_kv.nsrc)) {
-        case 4: k_sweep<4><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
-        case 9: k_sweep<9><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
-        case 16: k_sweep<16><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
-        case 20: k_sweep<20><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
-        default: k_sweep<32><<<grid, block, 0, stream>>>(d_kv, st, colour, iter); break;
-    }
+    ACMMP_LAUNCH_NS(k_sweep, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
     return hipGetLastError();
 }
 
@@ -1118,14 +1394,8 @@ hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &s
 
 hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float4 *planes, float *out,
                              float *out_init, uint32_t *out_views, hipStream_t stream) {
-    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
-    switch (ns_bucket(h_kv.nsrc)) {
-        case 4: k_eval_costs<4><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
-        case 9: k_eval_costs<9><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
-        case 16: k_eval_costs<16><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
-        case 20: k_eval_costs<20><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
-        default: k_eval_costs<32><<<grid, block, 0, stream>>>(d_kv, planes, out, out_init, out_views); break;
-    }
+    ACMMP_LAUNCH_NS(k_eval_costs, cs_grid(h_kv, 2), dim3(kBX, kBY), stream, d_kv, planes, out, out_init,
+                    out_views);
     return hipGetLastError();
 }
 

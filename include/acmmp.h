@@ -211,6 +211,12 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out);
 int acmmp_set_timing(acmmp_ctx *ctx, int enable);
 int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
 
+/* Hardware self-test: compares v_rcp_f32 + one Newton step with the IEEE
+ * division 1/z for every float32 in the fast-reciprocal exponent window
+ * (2^-125 <= |z| < 2^125). mismatches == 0 proves the ACMMP_FAST_RCP build
+ * bit-identical to the pinned division on this device. */
+int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked);
+
 /* Number of visible HIP devices (0 when none / no driver). */
 int acmmp_device_count(void);
 /* Library build string (arch, flags). */

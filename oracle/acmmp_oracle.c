@@ -20,8 +20,9 @@
  *   A6 --use_fast_math transcendentals -> include/acmmp_detmath.h.
  * Arithmetic pins shared with the HIP kernels (documented in DESIGN.md §4):
  *   P1 ComputeCorrespondingPoint (src/ACMMP.cu:324-331): each homogeneous
- *      coordinate is fma(H0,x,fma(H1,y,H2)); the divide is 1/z then two
- *      multiplies (what --use_fast_math's x*rcp(z) does, but exactly rounded).
+ *      coordinate is fma(H1,y,fma(H0,x,H2)) (the inner term is constant along
+ *      a patch column); the divide is 1/z then two multiplies (what
+ *      --use_fast_math's x*rcp(z) does, but exactly rounded).
  *   P2 bilinear: xs=(u+0.5)-0.5, clamp to [-1,W] by compare-select (NaN->-1),
  *      x0=floor, a=xs-x0, texels clamp-to-edge, lerp = fma(a, t1-t0, t0).
  *   P4 ComputeHomography (src/ACMMP.cu:292-311): x/w, x/K[0], x/K[4] are
@@ -350,9 +351,9 @@ static void ComputeHomography(const acmmp_camera *rc, const acmmp_camera *sc, co
 /* ComputeCorrespondingPoint (src/ACMMP.cu:324-331), pin P1 */
 static f2 ComputeCorrespondingPoint(const float *H, const i2 p) {
     const float x = (float)p.x, y = (float)p.y;
-    float ptx = dm_fma(H[0], x, dm_fma(H[1], y, H[2]));
-    float pty = dm_fma(H[3], x, dm_fma(H[4], y, H[5]));
-    float ptz = dm_fma(H[6], x, dm_fma(H[7], y, H[8]));
+    float ptx = dm_fma(H[1], y, dm_fma(H[0], x, H[2]));
+    float pty = dm_fma(H[4], y, dm_fma(H[3], x, H[5]));
+    float ptz = dm_fma(H[7], y, dm_fma(H[6], x, H[8]));
     float inv = 1.0f / ptz;
     f2 r = {ptx * inv, pty * inv};
     return r;

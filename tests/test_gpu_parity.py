@@ -196,3 +196,15 @@ def test_rng_stream_reseeds_second_run(small_scene):
     assert prm1.rng_stream == prm0.rng_stream + 1
     assert not np.array_equal(a, b)
     assert_bit_exact(b, oracle.run_patchmatch(prm1, cams, imgs)["planes"], "second run")
+
+
+def test_fast_reciprocal_is_exact_on_this_device():
+    """The sweep's fast 1/z (v_rcp_f32 + one fma Newton step) must equal the
+    IEEE division for EVERY float32 in its exponent window — the exhaustive
+    proof that makes the fast path bit-identical to the pinned semantics."""
+    import ctypes as C
+    from acmmp_amd import _abi
+    m, n = C.c_uint64(), C.c_uint64()
+    assert _abi.load_library().acmmp_selftest_reciprocal(0, C.byref(m), C.byref(n)) == 0
+    assert n.value == 2 * 250 * (1 << 23)  # both signs, exponents -125..124, all mantissas
+    assert m.value == 0
