@@ -299,8 +299,9 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
                        ctx->prm.patch_size, ctx->prm.radius_increment);
     for (int i = 0; i < num_images; ++i) {
         if (!images[i]) return set_err(ctx, ACMMP_ERR_ARG, "image %d is NULL", i);
-        if (cams[i].width <= 0 || cams[i].height <= 0)
-            return set_err(ctx, ACMMP_ERR_ARG, "camera %d has size %dx%d", i, cams[i].width, cams[i].height);
+        if (cams[i].width < 2 || cams[i].height < 1)
+            return set_err(ctx, ACMMP_ERR_ARG, "camera %d has size %dx%d (width >= 2 required)", i,
+                           cams[i].width, cams[i].height);
         if (borrow && pitches && pitches[i] < cams[i].width)
             return set_err(ctx, ACMMP_ERR_ARG, "image %d pitch %d < width %d", i, pitches[i], cams[i].width);
     }

@@ -208,3 +208,147 @@ def test_fast_reciprocal_is_exact_on_this_device():
     assert _abi.load_library().acmmp_selftest_reciprocal(0, C.byref(m), C.byref(n)) == 0
     assert n.value == 2 * 250 * (1 << 23)  # both signs, exponents -125..124, all mantissas
     assert m.value == 0
+
+
+def _cam_planes_from_truth(view, cam):
+    """Camera-frame plane hypotheses (n, d) from the analytic ground truth."""
+    H, W = view.depth.shape
+    K = np.array(cam.K).reshape(3, 3)
+    R = np.array(cam.R).reshape(3, 3)
+    n = view.normal @ R.T  # world -> camera
+    flip = n[..., 2] > 0
+    n[flip] *= -1
+    ys, xs = np.mgrid[0:H, 0:W]
+    z = np.where(view.depth > 0, view.depth, 600.0)
+    X = np.stack([z * (xs - K[0, 2]) / K[0, 0], z * (ys - K[1, 2]) / K[1, 1], z], -1)
+    d = -(n * X).sum(-1)
+    return np.concatenate([n, d[..., None]], -1).astype(np.float32)
+
+
+def test_planar_prior_second_run(small_scene):
+    """ProcessProblem's planar-prior flow (src/acmmp_definitions.cpp:306-379):
+    run, install triangle planes + label mask, SetPlanarPriorParams, run again
+    (random re-init + restricted propagation/refinement, src/ACMMP.cu:1095-1147,
+    :722-775)."""
+    cams, imgs = small_scene.problem(1, 4)
+    H, W = imgs[0].shape
+    planes_gt = _cam_planes_from_truth(small_scene.views[1], cams[0])
+    # 12 x 12 px "triangles": one plane per cell, taken from the cell centre;
+    # a band of unlabelled pixels keeps the mask > 0 / == 0 paths mixed
+    lab = (np.arange(H)[:, None] // 12) * ((W + 11) // 12) + (np.arange(W)[None, :] // 12)
+    mask = (lab + 1).astype(np.uint32)
+    mask[:, W // 2 - 3:W // 2 + 3] = 0
+    nlab = int(lab.max()) + 1
+    plane_params = np.zeros((nlab, 4), np.float32)
+    for l in range(nlab):
+        yy, xx = np.argwhere(lab == l)[len(np.argwhere(lab == l)) // 2]
+        plane_params[l] = planes_gt[yy, xx]
+    with ACMMP(0) as eng:
+        eng.set_params(_params(2))
+        eng.set_images(cams, imgs)
+        prm0 = eng.params
+        eng.RunPatchMatch()
+        first = (eng.plane_hypotheses(), eng.costs())
+        eng.SetPlanarPriorParams()
+        eng.CudaPlanarPriorInitialization(plane_params, mask)
+        prm1 = eng.params
+        eng.RunPatchMatch()
+        second = (eng.plane_hypotheses(), eng.costs(), eng.selected_views())
+    ref0 = oracle.run_patchmatch(prm0, cams, imgs)
+    assert_bit_exact(first[0], ref0["planes"], "first run planes")
+    per_pixel = np.where(mask[..., None] > 0, plane_params[np.maximum(mask.astype(np.int64) - 1, 0)], 0)
+    ref1 = oracle.run_patchmatch(prm1, cams, imgs, planes=ref0["planes"], costs=ref0["costs"],
+                                 prior_planes=per_pixel, masks=mask)
+    assert prm1.planar_prior == 1 and prm1.rng_stream == 1
+    assert_bit_exact(second[0], ref1["planes"], "planar-prior planes")
+    assert_bit_exact(second[1], ref1["costs"], "planar-prior costs")
+    assert_bit_exact(second[2], ref1["selected_views"], "planar-prior selected views")
+
+
+def test_planar_prior_init_branch_with_geom(small_scene):
+    """The planar-prior INIT branch (src/ACMMP.cu:640-661) is reachable only
+    with geom_consistency or hierarchy set; exercise it with geom."""
+    cams, imgs = small_scene.problem(2, 3)
+    ids = [2] + small_scene.pairs[2][:3]
+    depths = [small_scene.views[i].depth for i in ids]
+    H, W = imgs[0].shape
+    rng = np.random.default_rng(5)
+    state_planes = np.concatenate([small_scene.views[2].normal, small_scene.views[2].depth[..., None]], -1)
+    state_costs = rng.uniform(0, 0.3, size=(H, W)).astype(np.float32)
+    prior = _cam_planes_from_truth(small_scene.views[2], cams[0])
+    prior[..., 3] = small_scene.views[2].depth  # the init branch reads .w as a depth (:645)
+    mask = (rng.uniform(size=(H, W)) < 0.7).astype(np.uint32)
+    pp = prior.reshape(-1, 4)
+    labels = (np.arange(H * W) + 1).astype(np.uint32).reshape(H, W) * mask
+    p = _params(1)
+    p.geom_consistency = 1
+    p.planar_prior = 1
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        eng.set_depth_maps(depths)
+        eng.set_plane_hypotheses(state_planes, state_costs)
+        eng.CudaPlanarPriorInitialization(pp, labels)
+        prm = eng.params
+        eng.RunPatchMatch()
+        got = (eng.plane_hypotheses(), eng.costs())
+    per_pixel = np.where(mask[..., None] > 0, prior, 0).astype(np.float32)
+    ref = oracle.run_patchmatch(prm, cams, imgs, depths=depths, planes=state_planes, costs=state_costs,
+                                prior_planes=per_pixel, masks=labels)
+    assert_bit_exact(got[0], ref["planes"], "planes")
+    assert_bit_exact(got[1], ref["costs"], "costs")
+
+
+@pytest.mark.parametrize("same_size", [False, True])
+def test_hierarchy_init(small_scene, same_size):
+    """Hierarchical init (src/ACMMP.cpp:745-808, src/ACMMP.cu:663-703):
+    upsample branch (upscale_normal) from a half-resolution map, and the
+    non-upsample branch reached through the reference's rows/cols swap
+    (src/ACMMP.cpp:766), plus the hierarchy gate (:1163-1167)."""
+    cams, imgs = small_scene.problem(4, 4)
+    H, W = imgs[0].shape
+    rng = np.random.default_rng(9)
+    v = small_scene.views[4]
+    if same_size:
+        # scaled map "W x H" transposed-equal: the swap test says no upsample
+        sh, sw = W, H
+        scaled = np.zeros((sh, sw, 4), np.float32)
+        flat = np.concatenate([v.normal, v.depth[..., None]], -1).reshape(-1, 4)
+        scaled.reshape(-1, 4)[:] = flat
+    else:
+        sh, sw = H // 2, W // 2
+        scaled = np.concatenate([v.normal[::2, ::2], rng.uniform(0, 1, (sh, sw, 1))], -1).astype(np.float32)
+    up_depth = np.where(v.depth > 0, v.depth, 700.0).astype(np.float32)
+    p = _params(2)
+    p.hierarchy = 1
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        eng.set_hierarchy_inputs(scaled, up_depth)
+        prm = eng.params
+        eng.RunPatchMatch()
+        got = (eng.plane_hypotheses(), eng.costs())
+    assert prm.upsample == (0 if same_size else 1)
+    planes_in = np.zeros((H, W, 4), np.float32)
+    planes_in[..., 3] = up_depth
+    ref = oracle.run_patchmatch(prm, cams, imgs, planes=planes_in, pre_costs=np.zeros((H, W), np.float32),
+                                scaled_planes=scaled)
+    assert_bit_exact(got[0], ref["planes"], "planes")
+    assert_bit_exact(got[1], ref["costs"], "costs")
+
+
+def test_seeded_init(small_scene):
+    """Seeded priors (pSampler -> SetPlanarPrior, src/ACMMP.cu:634-639)."""
+    cams, imgs = small_scene.problem(5, 4)
+    seed = _cam_planes_from_truth(small_scene.views[5], cams[0])
+    with ACMMP(0) as eng:
+        eng.set_params(_params(2))
+        eng.set_images(cams, imgs)
+        eng.SetPlanarPrior(seed)
+        prm = eng.params
+        eng.RunPatchMatch()
+        got = (eng.plane_hypotheses(), eng.costs())
+    assert prm.seeded == 1
+    ref = oracle.run_patchmatch(prm, cams, imgs, seed_planes=seed)
+    assert_bit_exact(got[0], ref["planes"], "planes")
+    assert_bit_exact(got[1], ref["costs"], "costs")
