@@ -33,6 +33,9 @@ struct acmmp_ctx {
     std::vector<float *> own_img, own_dep;
     std::vector<const float *> img, dep;
     std::vector<int> img_pitch;
+    std::vector<float *> pad;          // padded source images (KViews::pad), owned
+    std::vector<size_t> pad_bytes;
+    std::vector<int> pad_pitch;
     std::vector<int> dep_pitch, dep_w, dep_h;
     bool have_depths = false;
 
@@ -180,6 +183,8 @@ int upload_kv(acmmp_ctx *ctx) {
         kv.cam[i] = ctx->cams[i];
         kv.img[i] = ctx->img[i];
         kv.ipitch[i] = ctx->img_pitch[i];
+        kv.pad[i] = ctx->pad[i];
+        kv.ppitch[i] = ctx->pad_pitch[i];
         if (i > 0) kv.rel[i] = view_rel(ctx->cams[0], ctx->cams[i]);
         if (ctx->have_depths) {
             kv.dep[i] = ctx->dep[i];
@@ -335,6 +340,23 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
             ctx->img[i] = ctx->own_img[i];
         }
     }
+    // clamp-to-edge padded copies of every view (device-side, stream ordered)
+    if (ctx->pad.size() < (size_t)num_images) {
+        ctx->pad.resize(num_images, nullptr);
+        ctx->pad_bytes.resize(num_images, 0);
+        ctx->pad_pitch.resize(num_images, 0);
+    }
+    for (int i = 0; i < num_images; ++i) {
+        const int w = cams[i].width, h = cams[i].height;
+        const int pp = (w + 3 + 31) / 32 * 32;
+        const size_t bytes = (size_t)pp * (h + 3) * sizeof(float);
+        if (ctx->pad_bytes[i] < bytes) {
+            HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
+            ctx->pad_bytes[i] = bytes;
+        }
+        ctx->pad_pitch[i] = pp;
+        HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
+    }
     if (resize || !ctx->d_rm_plane) {
         free_state(ctx);
         const size_t P = (size_t)ctx->W * ctx->H;
@@ -427,6 +449,7 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_images(ctx);
     free_state(ctx);
+    for (auto &p : ctx->pad) dfree(p);
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
         dfree(ctx->d_kv_ring[k]);
         if (ctx->h_kv_ring[k]) (void)hipHostFree(ctx->h_kv_ring[k]);
@@ -784,6 +807,11 @@ int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checke
     }
     (void)hipFree(d);
     return rc;
+}
+
+// Diagnostic builds only (ACMMP_DIAG_STAMPS); not declared in include/acmmp.h.
+int acmmp_diag_read_cycles(uint64_t *out8) {
+    return out8 ? diag_read_cycles((unsigned long long *)out8) : ACMMP_ERR_ARG;
 }
 
 int acmmp_set_timing(acmmp_ctx *ctx, int enable) {

@@ -36,6 +36,12 @@ struct KViews {
     ViewRel rel[ACMMP_MAX_IMAGES];            // rel[v] for source v (1-based), rel[0] unused
     const float *img[ACMMP_MAX_IMAGES];       // pitched images
     int ipitch[ACMMP_MAX_IMAGES];             // in floats
+    // Source images with clamp-to-edge baked in: element (r, c) holds texel
+    // (clamp(c - 1), clamp(r - 1)), (W + 3) x (H + 3), so every bilinear
+    // footprint of a coordinate clamped to [-1, W] x [-1, H] is addressable
+    // without integer clamps or selects.
+    const float *pad[ACMMP_MAX_IMAGES];
+    int ppitch[ACMMP_MAX_IMAGES];
     const float *dep[ACMMP_MAX_IMAGES];       // pitched depth maps (geom consistency)
     int dpitch[ACMMP_MAX_IMAGES];
     int dw[ACMMP_MAX_IMAGES];
@@ -75,6 +81,9 @@ hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float
 hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4 *planes,
                             float *out, hipStream_t stream);
 
+hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch,
+                            hipStream_t stream);
+int diag_read_cycles(unsigned long long *out8);
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);
 
 // Number of checkerboard rows the reference grid reaches (src/ACMMP.cu:1399).

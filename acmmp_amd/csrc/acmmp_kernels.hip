@@ -234,6 +234,11 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
 // replaces it, inside the exponent window below, by v_rcp_f32 + one fma
 // Newton step — used only if acmmp_selftest_reciprocal() proves the two
 // bit-identical for EVERY float in that window on this hardware.
+// Software-pipeline the NCC sample loop one patch column ahead (1) or
+// fetch-then-reduce each column (0; fewer VGPRs, latency hidden by waves).
+#ifndef ACMMP_NCC_PIPELINE
+#define ACMMP_NCC_PIPELINE 1
+#endif
 #ifndef ACMMP_FAST_RCP
 #define ACMMP_FAST_RCP 1
 #endif
@@ -264,9 +269,10 @@ DEV float2 project(const float *H, float x, float y) {
     return make_float2(px * inv, py * inv);
 }
 
-// Source-image sampler: one buffer resource (SRD) per view, built from
-// wave-uniform values (the view index is a uniform loop counter) so the
-// loads are `buffer_load_dwordx2 ... offen` with 32-bit offsets.
+// Source-image sampler: one buffer resource (SRD) per view over the padded
+// copy (KViews::pad), built from wave-uniform values (the view index is a
+// uniform loop counter) so the loads are `buffer_load_dwordx2 ... offen` with
+// 32-bit offsets and the row stride in the SGPR soffset.
 struct SrcImage {
     __amdgpu_buffer_rsrc_t rsrc;
     int pitch, W, H;
@@ -274,46 +280,14 @@ struct SrcImage {
 
 DEV SrcImage src_image(const KViews &kv, int v) {
     SrcImage s;
-    s.pitch = kv.ipitch[v];
+    s.pitch = kv.ppitch[v];
     s.W = kv.cam[v].width;
     s.H = kv.cam[v].height;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.img[v], (short)0, s.pitch * s.H * 4, 0x00020000);
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)0, s.pitch * (s.H + 3) * 4, 0x00020000);
     return s;
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// pin P2 (tex2D linear, clamp-to-edge; src/ACMMP.cu:394). The two texels of a
-// row are fetched as one 8-byte load at the clamped column pair
-// xb = clamp(x0, 0, W-2) and selected: for x0 in [-1, W] this reproduces
-// T[clamp(x0)], T[clamp(x0+1)] exactly (engine guarantees W >= 2).
-DEV float bilinear_buf(const SrcImage &im, float u, float v) {
-    float xs = (u + 0.5f) - 0.5f;
-    float ys = (v + 0.5f) - 0.5f;
-    const float fw = (float)im.W, fh = (float)im.H;
-    xs = (xs > -1.0f) ? xs : -1.0f;
-    xs = (xs < fw) ? xs : fw;
-    ys = (ys > -1.0f) ? ys : -1.0f;
-    ys = (ys < fh) ? ys : fh;
-    const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
-    const float ax = xs - fx0, ay = ys - fy0;
-    const int x0 = (int)fx0, y0 = (int)fy0;
-    int xb = x0 < 0 ? 0 : x0;
-    xb = xb > im.W - 2 ? im.W - 2 : xb;
-    const int ya = y0 < 0 ? 0 : (y0 > im.H - 1 ? im.H - 1 : y0);
-    const int yb = (y0 + 1) > (im.H - 1) ? (im.H - 1) : (y0 + 1 < 0 ? 0 : y0 + 1);
-    const u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (ya * im.pitch + xb) * 4, 0, 0);
-    const u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (yb * im.pitch + xb) * 4, 0, 0);
-    const bool lo_right = x0 >= im.W - 1;  // both texels are the last column
-    const bool hi_left = x0 < 0;           // both texels are the first column
-    const float t00 = __uint_as_float(lo_right ? r0.y : r0.x);
-    const float t10 = __uint_as_float(hi_left ? r0.x : r0.y);
-    const float t01 = __uint_as_float(lo_right ? r1.y : r1.x);
-    const float t11 = __uint_as_float(hi_left ? r1.x : r1.y);
-    const float top = dm_fma(ax, t10 - t00, t00);
-    const float bot = dm_fma(ax, t11 - t01, t01);
-    return dm_fma(ay, bot - top, top);
-}
 
 // ---------------------------------------------------------- ref-image tile
 // A block covers 64 colour-split columns (k0..k0+63) x 4 rows (y0..y0+3) of
@@ -342,11 +316,18 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // normalised ref mean / variance — identical for all 14*(N-1) calls of a
 // pixel-iteration, so computed once (same operations, same order).
 struct PixPatch {
-    float w[kSamples];
+    float *w;        // LDS: w[k * kThreads] for sample k of this lane (kThreads-strided)
+    int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
     float inv_wsum;  // inv_bilateral_weight_sum
 };
+
+// The 36 weights live in LDS, one 256-float row per sample index k, so a
+// wave's read of weight k is 64 consecutive dwords (conflict-free) and the
+// weights cost no VGPRs: 36 KB + the 3.9 KB tile per 256-thread block lets 4
+// blocks (16 waves) share a CU.
+constexpr int kThreads = kBX * kBY;
 
 DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
     const float spatial = dm_sqrt(xd * xd + yd * yd);
@@ -370,7 +351,7 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
-            pp.w[ii * kTaps + jj] = w;
+            pp.w[(ii * kTaps + jj) * kThreads] = w;
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -385,12 +366,13 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
 }
 
 // Fetch stage of one patch column (fixed x = px - 5 + 2 ii) of the source
-// samples: projection (pin P1, the x-term hoisted per column), clamp-to-edge
-// addressing (pin P2) and the two 8-byte texel-pair loads per sample.
+// samples: projection (pin P1, the x-term hoisted per column), the coordinate
+// clamp of pin P2, and two 8-byte texel-pair loads per sample from the padded
+// image (rows y0 and y0 + 1; padded element (y0 + 1, x0 + 1) is texel
+// (clamp(x0), clamp(y0))).
 struct ColFetch {
-    u32x2 t0[kTaps], t1[kTaps];  // texel pairs of rows clamp(y0), clamp(y0+1)
+    u32x2 t0[kTaps], t1[kTaps];  // texel pairs of rows y0, y0 + 1
     float ax[kTaps], ay[kTaps];   // bilinear weights
-    int x0[kTaps];                // floor column (selects the pair halves)
 };
 
 template <bool FAST>
@@ -399,6 +381,7 @@ DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFe
     const float cy = dm_fma(H[3], x, H[5]);
     const float cz = dm_fma(H[6], x, H[8]);
     const float fw = (float)im.W, fh = (float)im.H;
+    const int row_bytes = im.pitch * 4;
 #pragma unroll
     for (int jj = 0; jj < kTaps; ++jj) {
         const float y = (float)(py - 5 + 2 * jj);
@@ -415,13 +398,9 @@ DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFe
         const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
         f.ax[jj] = xs - fx0;
         f.ay[jj] = ys - fy0;
-        const int x0 = (int)fx0, y0 = (int)fy0;
-        f.x0[jj] = x0;
-        const int xb = min(max(x0, 0), im.W - 2);
-        const int ya = min(max(y0, 0), im.H - 1);
-        const int yb = min(y0 + 1, im.H - 1);  // y0 >= -1
-        f.t0[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (int)(__umul24(ya, im.pitch) + xb) * 4, 0, 0);
-        f.t1[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, (int)(__umul24(yb, im.pitch) + xb) * 4, 0, 0);
+        const int off = (int)(__umul24((unsigned)((int)fy0 + 1), (unsigned)im.pitch) + (unsigned)((int)fx0 + 1)) * 4;
+        f.t0[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, off, 0, 0);
+        f.t1[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, off, row_bytes, 0);
     }
 }
 
@@ -434,26 +413,35 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
     sum_src = 0.0f;
     sum_ss = 0.0f;
     sum_rs = 0.0f;
+    // re-read weights from LDS each call rather than caching them in VGPRs
+    // (launder the integer offset, not the pointer, so the LDS address space
+    // stays visible and the reads are ds_read, not flat)
+    int wo = pp.wo;
+    asm volatile("" : "+v"(wo));
+    const float *wl = pp.w - pp.wo + wo;
+#if ACMMP_NCC_PIPELINE
     ColFetch buf[2];
     fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
+#endif
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
+#if ACMMP_NCC_PIPELINE
         if (ii + 1 < kTaps) fetch_column<FAST>(im, H, (float)(px - 5 + 2 * (ii + 1)), py, buf[(ii + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         const ColFetch &f = buf[ii & 1];
+#else
+        ColFetch f;
+        fetch_column<FAST>(im, H, (float)(px - 5 + 2 * ii), py, f);
+#endif
         float r_s = 0.0f, r_ss = 0.0f, r_rs = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const bool lo_right = f.x0[jj] >= im.W - 1;  // both texels are the last column
-            const bool hi_left = f.x0[jj] < 0;           // both texels are the first column
-            const float t00 = __uint_as_float(lo_right ? f.t0[jj].y : f.t0[jj].x);
-            const float t10 = __uint_as_float(hi_left ? f.t0[jj].x : f.t0[jj].y);
-            const float t01 = __uint_as_float(lo_right ? f.t1[jj].y : f.t1[jj].x);
-            const float t11 = __uint_as_float(hi_left ? f.t1[jj].x : f.t1[jj].y);
+            const float t00 = __uint_as_float(f.t0[jj].x), t10 = __uint_as_float(f.t0[jj].y);
+            const float t01 = __uint_as_float(f.t1[jj].x), t11 = __uint_as_float(f.t1[jj].y);
             const float top = dm_fma(f.ax[jj], t10 - t00, t00);
             const float bot = dm_fma(f.ax[jj], t11 - t01, t01);
             const float sv = dm_fma(f.ay[jj], bot - top, top);
-            const float w = pp.w[ii * kTaps + jj];
+            const float w = wl[(ii * kTaps + jj) * kThreads];
             const float wr = w * tile[tb + ii + 2 * kTileW * jj];
             const float ws = w * sv;
             r_s += ws;
@@ -656,6 +644,19 @@ DEV float4 upscale_normal(const KViews &kv, const KState &st, int px, int py, fl
     return n_total;
 }
 
+// ------------------------------------------------- diagnostic phase stamps
+// ACMMP_DIAG_STAMPS builds only (never the product library): per-phase
+// s_memtime cycle sums of the sweep kernel, accumulated by lane 0 of each wave.
+#ifdef ACMMP_DIAG_STAMPS
+__device__ unsigned long long g_diag_cycles[8];
+#define DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(slot, a, b) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[slot], (b) - (a)); } while (0)
+#else
+#define DIAG_T(var)
+#define DIAG_ADD(slot, a, b)
+#endif
+
 // ------------------------------------------------------ colour-split lanes
 // Every PatchMatch kernel maps a 64x4 block onto 64 colour-split columns x 4
 // rows of ONE checkerboard colour: lane (tx, ty) of block (bx, by) handles
@@ -703,6 +704,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 template <int NS>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
+    __shared__ float wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -716,6 +718,8 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
     const int center = py * kv.W + px;
     dm_rng rs = make_rng(kv, center, 0u);
     PixPatch pp;
+    pp.wo = threadIdx.y * kBX + threadIdx.x;
+    pp.w = wlds + pp.wo;
     pixel_patch(kv, tile, g.tb, g.s, pp);
     float4 plane;
     float cost;
@@ -791,6 +795,8 @@ template <int NS>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
+    __shared__ float wlds[kSamples * kThreads];
+    DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
@@ -958,8 +964,12 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
 #undef CS
     auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
 
+    DIAG_T(t_search);
     PixPatch pp;
+    pp.wo = threadIdx.y * kBX + threadIdx.x;
+    pp.w = wlds + pp.wo;
     pixel_patch(kv, tile, g.tb, g.s, pp);
+    DIAG_T(t_patch);
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
@@ -972,6 +982,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         }
     }
 
+    DIAG_T(t_phaseA);
     // ---- multi-hypothesis joint view selection (:994-1056)
     float probs[NS];
     {
@@ -1057,6 +1068,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
             if (final_costs[i] <= m) { m = final_costs[i]; min_cost_idx = i; }
     }
 
+    DIAG_T(t_select);
     // ---- current hypothesis (:1080-1093) + refinement (:707-784): one NCC
     // site. t = 0 evaluates the current plane; t = 1..5 the refinement planes.
     const bool has_prior = prm.planar_prior && st.mask[center] > 0;
@@ -1215,6 +1227,12 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     st.plane_nx[colour][my] = my_plane;
     st.cost_nx[colour][my] = my_cost;
     st.sv[colour][my] = my_sv;
+    DIAG_T(t_end);
+    DIAG_ADD(0, t_start, t_search);
+    DIAG_ADD(1, t_search, t_patch);
+    DIAG_ADD(2, t_patch, t_phaseA);
+    DIAG_ADD(3, t_phaseA, t_select);
+    DIAG_ADD(4, t_select, t_end);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
@@ -1290,6 +1308,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
+    __shared__ float wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1299,6 +1318,8 @@ __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ k
     if (g.px >= kv.W || g.py >= kv.H) return;
     const int c = g.py * kv.W + g.px;
     PixPatch pp;
+    pp.wo = threadIdx.y * kBX + threadIdx.x;
+    pp.w = wlds + pp.wo;
     pixel_patch(kv, tile, g.tb, g.s, pp);
     const float4 h = planes[c];
     if (out)
@@ -1319,6 +1340,35 @@ __global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kv
     if (px >= kv.W || py >= kv.H) return;
     const int c = py * kv.W + px;
     for (int v = 0; v < kv.nsrc; ++v) out[(size_t)c * kv.nsrc + v] = geom_cost(kv, v + 1, planes[c], px, py);
+}
+
+// Padded copy of a source image (see KViews::pad).
+__global__ __launch_bounds__(256) void k_pad_image(const float *__restrict__ src, int spitch, int W, int H,
+                                                   float *__restrict__ dst, int dpitch) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int r = blockIdx.y * 4 + threadIdx.y;
+    if (c >= W + 3 || r >= H + 3) return;
+    const int x = min(max(c - 1, 0), W - 1), y = min(max(r - 1, 0), H - 1);
+    dst[r * dpitch + c] = src[y * spitch + x];
+}
+
+hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch, hipStream_t s) {
+    dim3 block(64, 4), grid((W + 3 + 63) / 64, (H + 3 + 3) / 4);
+    k_pad_image<<<grid, block, 0, s>>>(src, spitch, W, H, dst, dpitch);
+    return hipGetLastError();
+}
+
+int diag_read_cycles(unsigned long long *out8) {
+#ifdef ACMMP_DIAG_STAMPS
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -3;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_cycles), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+#else
+    (void)out8;
+    return -5;
+#endif
 }
 
 // Exhaustive check of recip_newton against IEEE 1/z over every float32 bit
