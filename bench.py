@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1200)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="400x300", help="ref-view crop timed on the CPU oracle")
+    ap.add_argument("--cpu-sample", default="800x600", help="ref-view crop timed on the CPU oracle")
     ap.add_argument("--profile-dir", default=None, help="write per-run timing JSON here")
     return ap.parse_args()
 
@@ -205,6 +205,8 @@ def main():
             "traffic": traffic,
             "model": "gather-byte model, SURVEY §8d: B_iter = 14*(N-1)*724 + 572 (+14*(N-1)*4 geom) "
                      "bytes per pixel-iteration, P/2 pixels per launch",
+            "note": "gather bytes are logical (counted as if uncached, BASELINE.md §3); frac > 1 means "
+                    "they are served from LDS/L1/L2 — traffic is the PMC-measured memory-side fetch+write",
             "sweep_launches": launches,
             "mean_launch_ms": round(sweep_ms / max(launches, 1), 3),
         },
