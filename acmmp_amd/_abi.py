@@ -107,6 +107,8 @@ _U32P = C.POINTER(C.c_uint32)
 _CTX = C.c_void_p
 
 # name -> (restype, argtypes)
+_I32P = C.POINTER(C.c_int32)
+
 SIGNATURES = {
     "acmmp_default_params": (None, [C.POINTER(Params)]),
     "acmmp_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -128,6 +130,11 @@ SIGNATURES = {
     "acmmp_set_hierarchy_inputs": (C.c_int, [_CTX, _FP, C.c_int, C.c_int, _FP]),
     "acmmp_set_seed_prior": (C.c_int, [_CTX, _FP]),
     "acmmp_set_planar_prior": (C.c_int, [_CTX, _FP, C.c_int, _U32P]),
+    "acmmp_get_support_points": (C.c_int, [_CTX, _I32P, C.c_int, C.POINTER(C.c_int)]),
+    "acmmp_delaunay_triangulation": (C.c_int, [C.c_int, C.c_int, _I32P, C.c_int, _I32P, C.c_int,
+                                               C.POINTER(C.c_int)]),
+    "acmmp_build_planar_prior": (C.c_int, [_CTX, _I32P, C.c_int, _FP, _U32P]),
+    "acmmp_prepare_planar_prior": (C.c_int, [_CTX, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_run_patchmatch": (C.c_int, [_CTX]),
     "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
     "acmmp_synchronize": (C.c_int, [_CTX]),

@@ -1,0 +1,120 @@
+// acmmp_ctx.h — the engine object behind the opaque `acmmp_ctx *` of
+// include/acmmp.h, shared by the translation units of libacmmp_amd.so
+// (acmmp_engine.hip: PatchMatch runs; acmmp_planar.hip: planar-prior
+// construction). Not installed, not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.h"
+#include "acmmp_internal.h"
+
+using namespace acmmp;
+
+struct acmmp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    acmmp_params prm{};
+    std::string err;
+
+    int n = 0;
+    int W = 0, H = 0, Wh = 0;
+    acmmp_camera cams[ACMMP_MAX_IMAGES]{};
+
+    // device buffers: images / depth maps are either owned (uploaded from the
+    // host, pitched) or borrowed (caller's device pointers, zero copy)
+    std::vector<float *> own_img, own_dep;
+    std::vector<const float *> img, dep;
+    std::vector<int> img_pitch;
+    std::vector<float *> pad;          // padded source images (KViews::pad), owned
+    std::vector<size_t> pad_bytes;
+    std::vector<int> pad_pitch;
+    std::vector<int> dep_pitch, dep_w, dep_h;
+    bool have_depths = false;
+
+    float4 *d_cplane[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [colour][pingpong]
+    float *d_ccost[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    uint32_t *d_csv[2] = {nullptr, nullptr};
+    int cur[2] = {0, 0};
+    float4 *d_rm_plane = nullptr;
+    float *d_rm_cost = nullptr;
+    uint32_t *d_rm_sv = nullptr;
+    float *d_pre_cost = nullptr;
+    float4 *d_prior = nullptr;
+    uint32_t *d_mask = nullptr;
+    float4 *d_scaled = nullptr;
+    size_t scaled_count = 0;
+    float4 *d_seed = nullptr;
+    bool have_prior = false, have_scaled = false, have_seed = false, have_state = false;
+
+    // Per-run constant block. A ring of pinned host / device slots so an
+    // asynchronous run never has its constants overwritten by the next
+    // enqueue: slot k is refilled only after its previous copy completed
+    // (event), and the device copy is stream-ordered behind the kernels that
+    // read it.
+    static constexpr int kSlots = 4;
+    KViews *d_kv_ring[kSlots] = {};
+    KViews *h_kv_ring[kSlots] = {};
+    hipEvent_t kv_ev[kSlots] = {};
+    bool kv_used[kSlots] = {};
+    int kv_slot = 0;
+    KViews *d_kv = nullptr;  // slot of the current enqueue
+    KViews h_kv{};
+
+    bool timing = false;
+    acmmp_timing last_timing{};
+    hipEvent_t ev[8] = {};
+    bool events_made = false;
+};
+
+namespace acmmp {
+
+
+inline int set_err(acmmp_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, ACMMP_ERR_HIP, "%s failed: %s (%s:%d)", #expr,               \
+                           hipGetErrorString(e_), __FILE__, __LINE__);                       \
+    } while (0)
+
+template <typename T>
+inline void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+template <typename T>
+inline hipError_t dalloc(T *&p, size_t count) {
+    dfree(p);
+    return hipMalloc((void **)&p, count * sizeof(T) > 0 ? count * sizeof(T) : 4);
+}
+
+inline int pitch_of(int w) { return (w + 63) / 64 * 64; }
+
+inline int check_ready(acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    if (ctx->n < 2) return set_err(ctx, ACMMP_ERR_STATE, "no images set (acmmp_set_images)");
+    return ACMMP_OK;
+}
+
+// Builds the KViews constant block for the next enqueue (acmmp_engine.hip).
+int upload_kv(acmmp_ctx *ctx);
+KState make_state(acmmp_ctx *ctx);
+
+}  // namespace acmmp

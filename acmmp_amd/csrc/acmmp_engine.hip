@@ -13,100 +13,10 @@
 #include <string>
 #include <vector>
 
-#include "../../include/acmmp.h"
-#include "acmmp_internal.h"
+#include "acmmp_ctx.h"
 
-using namespace acmmp;
-
-struct acmmp_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    acmmp_params prm{};
-    std::string err;
-
-    int n = 0;
-    int W = 0, H = 0, Wh = 0;
-    acmmp_camera cams[ACMMP_MAX_IMAGES]{};
-
-    // device buffers: images / depth maps are either owned (uploaded from the
-    // host, pitched) or borrowed (caller's device pointers, zero copy)
-    std::vector<float *> own_img, own_dep;
-    std::vector<const float *> img, dep;
-    std::vector<int> img_pitch;
-    std::vector<float *> pad;          // padded source images (KViews::pad), owned
-    std::vector<size_t> pad_bytes;
-    std::vector<int> pad_pitch;
-    std::vector<int> dep_pitch, dep_w, dep_h;
-    bool have_depths = false;
-
-    float4 *d_cplane[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [colour][pingpong]
-    float *d_ccost[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    uint32_t *d_csv[2] = {nullptr, nullptr};
-    int cur[2] = {0, 0};
-    float4 *d_rm_plane = nullptr;
-    float *d_rm_cost = nullptr;
-    uint32_t *d_rm_sv = nullptr;
-    float *d_pre_cost = nullptr;
-    float4 *d_prior = nullptr;
-    uint32_t *d_mask = nullptr;
-    float4 *d_scaled = nullptr;
-    size_t scaled_count = 0;
-    float4 *d_seed = nullptr;
-    bool have_prior = false, have_scaled = false, have_seed = false, have_state = false;
-
-    // Per-run constant block. A ring of pinned host / device slots so an
-    // asynchronous run never has its constants overwritten by the next
-    // enqueue: slot k is refilled only after its previous copy completed
-    // (event), and the device copy is stream-ordered behind the kernels that
-    // read it.
-    static constexpr int kSlots = 4;
-    KViews *d_kv_ring[kSlots] = {};
-    KViews *h_kv_ring[kSlots] = {};
-    hipEvent_t kv_ev[kSlots] = {};
-    bool kv_used[kSlots] = {};
-    int kv_slot = 0;
-    KViews *d_kv = nullptr;  // slot of the current enqueue
-    KViews h_kv{};
-
-    bool timing = false;
-    acmmp_timing last_timing{};
-    hipEvent_t ev[8] = {};
-    bool events_made = false;
-};
 
 namespace {
-
-int set_err(acmmp_ctx *ctx, int code, const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    if (ctx) ctx->err = buf;
-    return code;
-}
-
-#define HIP_TRY(ctx, expr)                                                                   \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess)                                                                \
-            return set_err(ctx, ACMMP_ERR_HIP, "%s failed: %s (%s:%d)", #expr,               \
-                           hipGetErrorString(e_), __FILE__, __LINE__);                       \
-    } while (0)
-
-template <typename T>
-void dfree(T *&p) {
-    if (p) (void)hipFree((void *)p);
-    p = nullptr;
-}
-
-template <typename T>
-hipError_t dalloc(T *&p, size_t count) {
-    dfree(p);
-    return hipMalloc((void **)&p, count * sizeof(T) > 0 ? count * sizeof(T) : 4);
-}
-
-int pitch_of(int w) { return (w + 63) / 64 * 64; }
 
 void free_depths(acmmp_ctx *ctx) {
     for (auto &p : ctx->own_dep) dfree(p);
@@ -176,7 +86,7 @@ ViewRel view_rel(const acmmp_camera &rc, const acmmp_camera &sc) {
 }
 
 // Rebuilds the device-side constant block from the context.
-int upload_kv(acmmp_ctx *ctx) {
+int kv_upload(acmmp_ctx *ctx) {
     KViews &kv = ctx->h_kv;
     kv.prm = ctx->prm;
     for (int i = 0; i < ctx->n; ++i) {
@@ -223,7 +133,7 @@ int upload_kv(acmmp_ctx *ctx) {
     return ACMMP_OK;
 }
 
-KState make_state(acmmp_ctx *ctx) {
+KState state_of(acmmp_ctx *ctx) {
     KState st{};
     for (int c = 0; c < 2; ++c) {
         st.plane[c] = ctx->d_cplane[c][ctx->cur[c]];
@@ -243,11 +153,6 @@ KState make_state(acmmp_ctx *ctx) {
     return st;
 }
 
-int check_ready(acmmp_ctx *ctx) {
-    if (!ctx) return ACMMP_ERR_ARG;
-    if (ctx->n < 2) return set_err(ctx, ACMMP_ERR_STATE, "no images set (acmmp_set_images)");
-    return ACMMP_OK;
-}
 
 int upload_pitched(acmmp_ctx *ctx, float *&dst, int &pitch, const float *src, int w, int h, bool device_src) {
     pitch = pitch_of(w);
@@ -391,6 +296,11 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 }
 
 }  // namespace
+
+namespace acmmp {
+int upload_kv(acmmp_ctx *ctx) { return kv_upload(ctx); }
+KState make_state(acmmp_ctx *ctx) { return state_of(ctx); }
+}  // namespace acmmp
 
 extern "C" {
 
@@ -636,7 +546,7 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
         return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "only patch_size 11 / radius_increment 2 are built");
     if (p.max_iterations < 0) return set_err(ctx, ACMMP_ERR_ARG, "max_iterations < 0");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    rc = upload_kv(ctx);
+    rc = kv_upload(ctx);
     if (rc) return rc;
     if (ctx->timing && !ctx->events_made) {
         for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
@@ -645,18 +555,18 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     hipStream_t s = ctx->stream;
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
     ctx->cur[0] = ctx->cur[1] = 0;
-    HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, make_state(ctx), s));
+    HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
     for (int it = 0; it < p.max_iterations; ++it) {
         for (int colour = 0; colour < 2; ++colour) {  // BlackPixelUpdate, RedPixelUpdate
-            HIP_TRY(ctx, launch_sweep(ctx->d_kv, ctx->h_kv, make_state(ctx), colour, it, s));
+            HIP_TRY(ctx, launch_sweep(ctx->d_kv, ctx->h_kv, state_of(ctx), colour, it, s));
             ctx->cur[colour] ^= 1;
         }
     }
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
-    HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, make_state(ctx), s));
-    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, make_state(ctx), 0, s));
-    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, make_state(ctx), 1, s));
+    HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 0, s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 1, s));
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
     ctx->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
     ctx->have_state = true;
@@ -740,7 +650,7 @@ int acmmp_eval_costs(acmmp_ctx *ctx, const float *planes4, float *out_costs, flo
     if (rc) return rc;
     if (!planes4) return set_err(ctx, ACMMP_ERR_ARG, "planes NULL");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    rc = upload_kv(ctx);
+    rc = kv_upload(ctx);
     if (rc) return rc;
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;
@@ -773,7 +683,7 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
     if (!planes4 || !out) return set_err(ctx, ACMMP_ERR_ARG, "NULL argument");
     if (!ctx->have_depths) return set_err(ctx, ACMMP_ERR_STATE, "no depth maps");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    rc = upload_kv(ctx);
+    rc = kv_upload(ctx);
     if (rc) return rc;
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;

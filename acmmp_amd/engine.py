@@ -43,6 +43,26 @@ def _uptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_uint32))
 
 
+def _iptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def delaunay_triangulation(width: int, height: int, points: np.ndarray) -> np.ndarray:
+    """DelaunayTriangulation (src/ACMMP.cpp:896-918): exact Delaunay of integer
+    points in [0,width) x [0,height); (m, 6) int32 triangles x1 y1 x2 y2 x3 y3,
+    only those with all corners in the image. Host code, no GPU needed."""
+    lib = _abi.load_library()
+    pts = np.ascontiguousarray(points, dtype=np.int32).reshape(-1, 2)
+    cap = 2 * pts.shape[0] + 16
+    tris = np.empty((cap, 6), dtype=np.int32)
+    n = C.c_int(0)
+    rc = lib.acmmp_delaunay_triangulation(int(width), int(height), _iptr(pts), int(pts.shape[0]), _iptr(tris),
+                                          cap, C.byref(n))
+    if rc != 0:
+        raise AcmmpError(f"acmmp_delaunay_triangulation failed (status {rc})")
+    return tris[: n.value].copy()
+
+
 def device_count() -> int:
     return int(_abi.load_library().acmmp_device_count())
 
@@ -190,6 +210,42 @@ class ACMMP:
         mk = np.ascontiguousarray(mask, dtype=np.uint32)
         self._check(self._lib.acmmp_set_planar_prior(self._ctx, _fptr(pp), int(pp.shape[0]), _uptr(mk)),
                     "CudaPlanarPriorInitialization")
+
+    # ------------------------------------------------- planar prior (a17)
+    def GetSupportPoints(self) -> np.ndarray:
+        """src/ACMMP.cpp:868-894 on the resident results: (n, 2) int32 (x, y)."""
+        w, h = self.size
+        cap = (w // 5 + 1) * (h // 5 + 1)
+        xy = np.empty((cap, 2), dtype=np.int32)
+        n = C.c_int(0)
+        self._check(self._lib.acmmp_get_support_points(self._ctx, _iptr(xy), cap, C.byref(n)), "GetSupportPoints")
+        return xy[: n.value].copy()
+
+    def DelaunayTriangulation(self, points: np.ndarray) -> np.ndarray:
+        """src/ACMMP.cpp:896-918 over this view's image rectangle."""
+        w, h = self.size
+        return delaunay_triangulation(w, h, points)
+
+    def build_planar_prior(self, triangles: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """Raster + GetPriorPlaneParams + range check + CudaPlanarPriorInitialization
+        (src/acmmp_definitions.cpp:332-376) on the device; returns the fitted
+        planes (one float4 per in-image triangle) and the final label mask."""
+        w, h = self.size
+        tr = np.ascontiguousarray(triangles, dtype=np.int32).reshape(-1, 6)
+        planes = np.empty((max(tr.shape[0], 1), 4), dtype=np.float32)
+        mask = np.empty((h, w), dtype=np.uint32)
+        self._check(self._lib.acmmp_build_planar_prior(self._ctx, _iptr(tr), int(tr.shape[0]), _fptr(planes),
+                                                       _uptr(mask)), "acmmp_build_planar_prior")
+        inside = ((tr[:, 0::2] >= 0) & (tr[:, 0::2] < w) & (tr[:, 1::2] >= 0) & (tr[:, 1::2] < h)).all(axis=1)
+        return planes[: int(inside.sum())], mask
+
+    def prepare_planar_prior(self) -> tuple[int, int]:
+        """Support points -> Delaunay -> prior build -> SetPlanarPriorParams.
+        Returns (support points, triangles)."""
+        npts, ntri = C.c_int(0), C.c_int(0)
+        self._check(self._lib.acmmp_prepare_planar_prior(self._ctx, C.byref(npts), C.byref(ntri)),
+                    "acmmp_prepare_planar_prior")
+        return npts.value, ntri.value
 
     # ----------------------------------------------------------------- run
     def RunPatchMatch(self):

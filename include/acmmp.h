@@ -164,6 +164,36 @@ int acmmp_set_seed_prior(acmmp_ctx *ctx, const float *planes4);
 int acmmp_set_planar_prior(acmmp_ctx *ctx, const float *plane_params4, int num_planes,
                            const uint32_t *mask);
 
+/* ~ ACMMP::GetSupportPoints (src/ACMMP.cpp:868-894) on the resident results
+ * of the last run: per 5x5 block (col-major block order) the pixel of lowest
+ * cost < 2, kept if that cost < 0.1. Writes (x, y) pairs; *count = number
+ * found (ACMMP_ERR_ARG if it exceeds capacity). */
+int acmmp_get_support_points(acmmp_ctx *ctx, int32_t *xy, int capacity, int *count);
+
+/* ~ ACMMP::DelaunayTriangulation (src/ACMMP.cpp:896-918): host-side exact
+ * Delaunay triangulation of integer points inside [0,width) x [0,height)
+ * (cv::Subdiv2D's bounding triangle, strict in-circle ties). Writes the
+ * triangles with all three corners in the image, 6 int32 each
+ * (x1 y1 x2 y2 x3 y3); needs no context or GPU. */
+int acmmp_delaunay_triangulation(int width, int height, const int32_t *xy, int num_points, int32_t *tris,
+                                 int capacity, int *num_triangles);
+
+/* The planar-prior block of ProcessProblem (src/acmmp_definitions.cpp:332-376):
+ * triangle raster into a label mask, ACMMP::GetPriorPlaneParams per triangle
+ * (src/ACMMP.cpp:920-953) fitted to the resident depth map,
+ * GetDepthFromPlaneParam range check (:955-958) and
+ * CudaPlanarPriorInitialization (:811-831), all on the device. Optional
+ * outputs: the fitted planes (float4 per kept triangle) and the final label
+ * mask (W*H). Does not set params.planar_prior. */
+int acmmp_build_planar_prior(acmmp_ctx *ctx, const int32_t *tris, int num_triangles, float *out_planes4,
+                             uint32_t *out_mask);
+
+/* Support points -> Delaunay -> acmmp_build_planar_prior ->
+ * SetPlanarPriorParams (src/ACMMP.cpp:456-459), i.e. everything ProcessProblem
+ * does between its two RunPatchMatch calls except the triangulation.png
+ * drawing. */
+int acmmp_prepare_planar_prior(acmmp_ctx *ctx, int *num_support_points, int *num_triangles);
+
 /* ~ ACMMP::RunPatchMatch (src/ACMMP.cu:1378-1456): init, max_iterations x
  * (black, red) checkerboard sweeps, depth/normal conversion, black/red median
  * filter. Results stay resident on the device; then rng_stream += 1. */

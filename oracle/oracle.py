@@ -60,6 +60,14 @@ def _load():
         fn.argtypes = [C.c_float]
     lib.acmmp_oracle_checkerboard_rows.restype = C.c_int
     lib.acmmp_oracle_checkerboard_rows.argtypes = [C.c_int]
+    I32P = C.POINTER(C.c_int32)
+    lib.acmmp_oracle_support_points.restype = C.c_int
+    lib.acmmp_oracle_support_points.argtypes = [FP, C.c_int, C.c_int, I32P]
+    lib.acmmp_oracle_prior_plane.restype = None
+    lib.acmmp_oracle_prior_plane.argtypes = [CAM, FP, C.c_int, I32P, FP]
+    lib.acmmp_oracle_planar_prior.restype = None
+    lib.acmmp_oracle_planar_prior.argtypes = [CAM, FP, C.c_int, C.c_int, C.c_float, C.c_float, I32P, C.c_int,
+                                              FP, U32P, FP]
     _lib = lib
     return lib
 
@@ -182,3 +190,33 @@ def math_fn(name, x):
 
 def checkerboard_rows(H):
     return int(_load().acmmp_oracle_checkerboard_rows(int(H)))
+
+
+def _i(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def support_points(costs):
+    """GetSupportPoints (src/ACMMP.cpp:868-894) on a (H, W) cost map."""
+    lib = _load()
+    c = np.ascontiguousarray(costs, dtype=np.float32)
+    h, w = c.shape
+    out = np.empty(((w // 5 + 1) * (h // 5 + 1), 2), dtype=np.int32)
+    n = lib.acmmp_oracle_support_points(_f(c), w, h, _i(out))
+    return out[:n].copy()
+
+
+def planar_prior(cam, depths, depth_min, depth_max, triangles):
+    """Raster + GetPriorPlaneParams + range check + label expansion
+    (src/acmmp_definitions.cpp:332-370, src/ACMMP.cpp:811-831, 920-958) for a
+    triangle list already restricted to the image. Returns (planes, mask, prior)."""
+    lib = _load()
+    d = np.ascontiguousarray(depths, dtype=np.float32)
+    h, w = d.shape
+    tr = np.ascontiguousarray(triangles, dtype=np.int32).reshape(-1, 6)
+    planes = np.zeros((max(tr.shape[0], 1), 4), dtype=np.float32)
+    mask = np.zeros((h, w), dtype=np.uint32)
+    prior = np.zeros((h, w, 4), dtype=np.float32)
+    lib.acmmp_oracle_planar_prior(C.byref(cam), _f(d), w, h, float(depth_min), float(depth_max), _i(tr),
+                                  int(tr.shape[0]), _f(planes), _u(mask), _f(prior))
+    return planes[: tr.shape[0]], mask, prior
