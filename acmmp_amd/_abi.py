@@ -151,6 +151,9 @@ SIGNATURES = {
     "acmmp_selftest_reciprocal": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "acmmp_device_count": (C.c_int, []),
     "acmmp_version": (C.c_char_p, []),
+    "acmmp_read_image_gray": (C.c_int, [C.c_char_p, _FP, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "acmmp_image_size": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "acmmp_resize_linear": (C.c_int, [_FP, C.c_int, C.c_int, _FP, C.c_int, C.c_int]),
     "acmmp_read_camera": (C.c_int, [C.c_char_p, C.POINTER(Camera)]),
     "acmmp_read_dmb": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                  C.POINTER(C.c_int32), _FP, C.c_size_t]),

@@ -1,0 +1,624 @@
+// acmmp_image.cpp — grayscale image input for InputInitialization
+// (src/ACMMP.cpp:525-601) without OpenCV:
+//
+//  * cv::imread(path, IMREAD_GRAYSCALE) of the reference's `%08d.jpg` inputs:
+//    a baseline (SOF0/SOF1, 8-bit, Huffman) JPEG decoder that returns the
+//    luminance plane exactly as libjpeg's JCS_GRAYSCALE output does — the
+//    ISLOW integer IDCT with its range-limit table, Y taken without colour
+//    conversion. Progressive / arithmetic / 12-bit files are rejected
+//    (ACMMP_ERR_UNSUPPORTED).
+//  * binary PGM (P5, 8/16-bit) and grayscale PFM as lossless alternatives.
+//  * cv::resize(..., INTER_LINEAR) of a float image (src/ACMMP.cpp:578-597),
+//    including OpenCV's switch to INTER_AREA for exact 2x downscales.
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.h"
+
+namespace {
+
+bool read_file(const char *path, std::vector<uint8_t> &buf) {
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    if (n < 0) {
+        std::fclose(f);
+        return false;
+    }
+    buf.resize((size_t)n);
+    bool ok = n == 0 || std::fread(buf.data(), 1, (size_t)n, f) == (size_t)n;
+    std::fclose(f);
+    return ok;
+}
+
+// ------------------------------------------------------------------ JPEG
+struct Huff {
+    // canonical decoding tables: maxcode[l], valptr[l], mincode[l]
+    int32_t mincode[17], maxcode[18], valptr[17];
+    uint8_t vals[256];
+    bool present = false;
+};
+
+struct Comp {
+    int id, h, v, tq;
+    int td = 0, ta = 0;
+    int bw = 0, bh = 0;         // blocks per line / column (component extent, padded to MCU)
+    std::vector<int16_t> coef;  // only for the luminance component
+    int pred = 0;
+};
+
+struct Jpeg {
+    const uint8_t *p = nullptr, *end = nullptr;
+    int W = 0, H = 0, ncomp = 0, hmax = 1, vmax = 1;
+    Comp comp[4];
+    uint16_t qt[4][64];
+    bool qt_present[4] = {false, false, false, false};
+    Huff dc[4], ac[4];
+    int restart = 0;
+    bool sof = false;
+    // bit reader
+    uint32_t bitbuf = 0;
+    int bitcnt = 0;
+    bool hit_marker = false;
+
+    int err = ACMMP_OK;
+};
+
+const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+int u16(const uint8_t *q) { return (q[0] << 8) | q[1]; }
+
+bool build_huff(Huff &h, const uint8_t *counts, const uint8_t *symbols, int nsym) {
+    if (nsym > 256) return false;
+    std::memcpy(h.vals, symbols, nsym);
+    int code = 0, k = 0;
+    for (int l = 1; l <= 16; ++l) {
+        h.valptr[l] = k;
+        h.mincode[l] = code;
+        code += counts[l - 1];
+        k += counts[l - 1];
+        h.maxcode[l] = counts[l - 1] ? code - 1 : -1;
+        code <<= 1;
+    }
+    h.maxcode[17] = 0x7fffffff;
+    h.present = true;
+    return true;
+}
+
+// Fill the bit buffer; after a marker, feed zeros (libjpeg behaviour).
+inline void fill(Jpeg &j) {
+    while (j.bitcnt <= 24) {
+        int byte = 0;
+        if (!j.hit_marker && j.p < j.end) {
+            byte = *j.p;
+            if (byte == 0xFF) {
+                const int nx = (j.p + 1 < j.end) ? j.p[1] : 0;
+                if (nx == 0x00) {
+                    j.p += 2;
+                } else {
+                    j.hit_marker = true;  // leave the marker for the caller
+                    byte = 0;
+                }
+            } else {
+                ++j.p;
+            }
+        }
+        j.bitbuf |= (uint32_t)byte << (24 - j.bitcnt);
+        j.bitcnt += 8;
+    }
+}
+
+inline int getbits(Jpeg &j, int n) {
+    if (n == 0) return 0;
+    fill(j);
+    const int v = (int)(j.bitbuf >> (32 - n));
+    j.bitbuf <<= n;
+    j.bitcnt -= n;
+    return v;
+}
+
+inline int decode_huff(Jpeg &j, const Huff &h) {
+    fill(j);
+    int code = 0;
+    for (int l = 1; l <= 16; ++l) {
+        code = (code << 1) | (int)(j.bitbuf >> 31);
+        j.bitbuf <<= 1;
+        j.bitcnt -= 1;
+        if (h.maxcode[l] >= 0 && code <= h.maxcode[l] && code >= h.mincode[l])
+            return h.vals[h.valptr[l] + code - h.mincode[l]];
+    }
+    j.err = ACMMP_ERR_IO;  // corrupt data
+    return 0;
+}
+
+inline int extend(int v, int t) { return (t && v < (1 << (t - 1))) ? v - (1 << t) + 1 : v; }
+
+void decode_block(Jpeg &j, Comp &c, int16_t *out) {
+    const int t = decode_huff(j, j.dc[c.td]);
+    if (t > 16) {
+        j.err = ACMMP_ERR_IO;
+        return;
+    }
+    const int diff = extend(getbits(j, t), t);
+    c.pred += diff;
+    if (out) {
+        std::memset(out, 0, 64 * sizeof(int16_t));
+        out[0] = (int16_t)c.pred;
+    }
+    for (int k = 1; k < 64;) {
+        const int rs = decode_huff(j, j.ac[c.ta]);
+        const int r = rs >> 4, s = rs & 15;
+        if (s == 0) {
+            if (r != 15) break;  // EOB
+            k += 16;
+            continue;
+        }
+        k += r;
+        const int v = extend(getbits(j, s), s);
+        if (k > 63) {
+            j.err = ACMMP_ERR_IO;
+            return;
+        }
+        if (out) out[kZigzag[k]] = (int16_t)v;
+        ++k;
+    }
+}
+
+// Skip to the restart marker and reset the entropy decoder.
+void handle_restart(Jpeg &j) {
+    j.bitbuf = 0;
+    j.bitcnt = 0;
+    j.hit_marker = false;
+    while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] >= 0xD0 && j.p[1] <= 0xD7)) ++j.p;
+    if (j.p + 1 < j.end) j.p += 2;
+    for (int c = 0; c < j.ncomp; ++c) j.comp[c].pred = 0;
+}
+
+bool decode_scan(Jpeg &j, const uint8_t *hdr, int len) {
+    const int ns = hdr[0];
+    if (ns < 1 || ns > 4 || len < 1 + 2 * ns + 3) return false;
+    int sc[4];
+    for (int i = 0; i < ns; ++i) {
+        const int cid = hdr[1 + 2 * i], tbl = hdr[2 + 2 * i];
+        sc[i] = -1;
+        for (int c = 0; c < j.ncomp; ++c)
+            if (j.comp[c].id == cid) sc[i] = c;
+        if (sc[i] < 0) return false;
+        j.comp[sc[i]].td = tbl >> 4;
+        j.comp[sc[i]].ta = tbl & 15;
+        if (j.comp[sc[i]].td > 3 || j.comp[sc[i]].ta > 3 || !j.dc[j.comp[sc[i]].td].present ||
+            !j.ac[j.comp[sc[i]].ta].present)
+            return false;
+    }
+    const int ss = hdr[1 + 2 * ns], se = hdr[2 + 2 * ns], ahal = hdr[3 + 2 * ns];
+    if (ss != 0 || se != 63 || ahal != 0) return false;  // sequential only
+    for (int i = 0; i < ns; ++i) j.comp[sc[i]].pred = 0;
+    j.bitbuf = 0;
+    j.bitcnt = 0;
+    j.hit_marker = false;
+    int mcus_x, mcus_y;
+    if (ns == 1) {
+        const Comp &c = j.comp[sc[0]];
+        mcus_x = (int)((j.W * (long)c.h + 8L * j.hmax - 1) / (8L * j.hmax));
+        mcus_y = (int)((j.H * (long)c.v + 8L * j.vmax - 1) / (8L * j.vmax));
+    } else {
+        mcus_x = (j.W + 8 * j.hmax - 1) / (8 * j.hmax);
+        mcus_y = (j.H + 8 * j.vmax - 1) / (8 * j.vmax);
+    }
+    int todo = j.restart;
+    for (int my = 0; my < mcus_y; ++my) {
+        for (int mx = 0; mx < mcus_x; ++mx) {
+            if (j.restart && todo == 0) {
+                handle_restart(j);
+                todo = j.restart;
+            }
+            for (int i = 0; i < ns; ++i) {
+                Comp &c = j.comp[sc[i]];
+                const int bx_n = ns == 1 ? 1 : c.h, by_n = ns == 1 ? 1 : c.v;
+                for (int by = 0; by < by_n; ++by)
+                    for (int bx = 0; bx < bx_n; ++bx) {
+                        const int gx = ns == 1 ? mx : mx * c.h + bx;
+                        const int gy = ns == 1 ? my : my * c.v + by;
+                        int16_t *dst = nullptr;
+                        if (sc[i] == 0 && gx < c.bw && gy < c.bh) dst = &c.coef[((size_t)gy * c.bw + gx) * 64];
+                        decode_block(j, c, dst);
+                        if (j.err) return false;
+                    }
+            }
+            if (j.restart) --todo;
+        }
+    }
+    // continue after the entropy-coded segment
+    while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] != 0x00 && !(j.p[1] >= 0xD0 && j.p[1] <= 0xD7))) ++j.p;
+    return true;
+}
+
+// jpeg_idct_islow (libjpeg jidctint.c): 13-bit fixed point, PASS1_BITS = 2.
+constexpr int kConstBits = 13, kPass1Bits = 2;
+constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633,
+                  F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
+
+inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+
+inline uint8_t range_limit(int32_t x) {
+    const int idx = x & 1023;  // RANGE_MASK of the post-IDCT table (jdmaster.c)
+    if (idx < 128) return (uint8_t)(idx + 128);
+    if (idx < 512) return 255;
+    if (idx < 896) return 0;
+    return (uint8_t)(idx - 896);
+}
+
+void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) {
+    int32_t ws[64];
+    for (int c = 0; c < 8; ++c) {
+        const int16_t *ip = in + c;
+        const uint16_t *qp = q + c;
+        if (!ip[8] && !ip[16] && !ip[24] && !ip[32] && !ip[40] && !ip[48] && !ip[56]) {
+            const int32_t dc = ((int32_t)ip[0] * qp[0]) << kPass1Bits;
+            for (int r = 0; r < 8; ++r) ws[r * 8 + c] = dc;
+            continue;
+        }
+        int32_t z2 = (int32_t)ip[16] * qp[16], z3 = (int32_t)ip[48] * qp[48];
+        int32_t z1 = (z2 + z3) * F0541;
+        int32_t tmp2 = z1 + z3 * (-F1847);
+        int32_t tmp3 = z1 + z2 * F0765;
+        z2 = (int32_t)ip[0] * qp[0];
+        z3 = (int32_t)ip[32] * qp[32];
+        int32_t tmp0 = (z2 + z3) * (1 << kConstBits);
+        int32_t tmp1 = (z2 - z3) * (1 << kConstBits);
+        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = (int32_t)ip[56] * qp[56];
+        tmp1 = (int32_t)ip[40] * qp[40];
+        tmp2 = (int32_t)ip[24] * qp[24];
+        tmp3 = (int32_t)ip[8] * qp[8];
+        z1 = tmp0 + tmp3;
+        z2 = tmp1 + tmp2;
+        z3 = tmp0 + tmp2;
+        int32_t z4 = tmp1 + tmp3;
+        const int32_t z5 = (z3 + z4) * F1175;
+        tmp0 *= F0298;
+        tmp1 *= F2053;
+        tmp2 *= F3072;
+        tmp3 *= F1501;
+        z1 *= -F0899;
+        z2 *= -F2562;
+        z3 *= -F1961;
+        z4 *= -F0390;
+        z3 += z5;
+        z4 += z5;
+        tmp0 += z1 + z3;
+        tmp1 += z2 + z4;
+        tmp2 += z2 + z3;
+        tmp3 += z1 + z4;
+        const int sh = kConstBits - kPass1Bits;
+        ws[0 * 8 + c] = descale(tmp10 + tmp3, sh);
+        ws[7 * 8 + c] = descale(tmp10 - tmp3, sh);
+        ws[1 * 8 + c] = descale(tmp11 + tmp2, sh);
+        ws[6 * 8 + c] = descale(tmp11 - tmp2, sh);
+        ws[2 * 8 + c] = descale(tmp12 + tmp1, sh);
+        ws[5 * 8 + c] = descale(tmp12 - tmp1, sh);
+        ws[3 * 8 + c] = descale(tmp13 + tmp0, sh);
+        ws[4 * 8 + c] = descale(tmp13 - tmp0, sh);
+    }
+    const int sh = kConstBits + kPass1Bits + 3;
+    for (int r = 0; r < 8; ++r) {
+        const int32_t *w = ws + r * 8;
+        uint8_t *o = out + (size_t)r * stride;
+        int32_t z2 = w[2], z3 = w[6];
+        int32_t z1 = (z2 + z3) * F0541;
+        int32_t tmp2 = z1 + z3 * (-F1847);
+        int32_t tmp3 = z1 + z2 * F0765;
+        int32_t tmp0 = (w[0] + w[4]) * (1 << kConstBits);
+        int32_t tmp1 = (w[0] - w[4]) * (1 << kConstBits);
+        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = w[7];
+        tmp1 = w[5];
+        tmp2 = w[3];
+        tmp3 = w[1];
+        z1 = tmp0 + tmp3;
+        z2 = tmp1 + tmp2;
+        z3 = tmp0 + tmp2;
+        int32_t z4 = tmp1 + tmp3;
+        const int32_t z5 = (z3 + z4) * F1175;
+        tmp0 *= F0298;
+        tmp1 *= F2053;
+        tmp2 *= F3072;
+        tmp3 *= F1501;
+        z1 *= -F0899;
+        z2 *= -F2562;
+        z3 *= -F1961;
+        z4 *= -F0390;
+        z3 += z5;
+        z4 += z5;
+        tmp0 += z1 + z3;
+        tmp1 += z2 + z4;
+        tmp2 += z2 + z3;
+        tmp3 += z1 + z4;
+        o[0] = range_limit(descale(tmp10 + tmp3, sh));
+        o[7] = range_limit(descale(tmp10 - tmp3, sh));
+        o[1] = range_limit(descale(tmp11 + tmp2, sh));
+        o[6] = range_limit(descale(tmp11 - tmp2, sh));
+        o[2] = range_limit(descale(tmp12 + tmp1, sh));
+        o[5] = range_limit(descale(tmp12 - tmp1, sh));
+        o[3] = range_limit(descale(tmp13 + tmp0, sh));
+        o[4] = range_limit(descale(tmp13 - tmp0, sh));
+    }
+}
+
+// Parses markers up to the first SOS (size_only) or decodes the luminance
+// plane into `gray` (W*H bytes).
+int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H, std::vector<uint8_t> *gray) {
+    Jpeg j;
+    j.p = buf.data();
+    j.end = buf.data() + buf.size();
+    if (buf.size() < 4 || j.p[0] != 0xFF || j.p[1] != 0xD8) return ACMMP_ERR_IO;
+    j.p += 2;
+    bool decoded = false;
+    while (j.p + 4 <= j.end) {
+        if (j.p[0] != 0xFF) {
+            ++j.p;
+            continue;
+        }
+        const int m = j.p[1];
+        j.p += 2;
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01 || m == 0xFF) {
+            if (m == 0xFF) --j.p;
+            continue;
+        }
+        if (m == 0xD9) break;  // EOI
+        if (j.p + 2 > j.end) return ACMMP_ERR_IO;
+        const int len = u16(j.p);
+        const uint8_t *seg = j.p + 2;
+        if (len < 2 || j.p + len > j.end) return ACMMP_ERR_IO;
+        j.p += len;
+        const int n = len - 2;
+        if (m == 0xC0 || m == 0xC1) {  // baseline / extended sequential Huffman
+            if (n < 6 || seg[0] != 8) return ACMMP_ERR_UNSUPPORTED;
+            j.H = u16(seg + 1);
+            j.W = u16(seg + 3);
+            j.ncomp = seg[5];
+            if (j.ncomp < 1 || j.ncomp > 4 || n < 6 + 3 * j.ncomp || j.W <= 0 || j.H <= 0) return ACMMP_ERR_UNSUPPORTED;
+            for (int c = 0; c < j.ncomp; ++c) {
+                Comp &cp = j.comp[c];
+                cp.id = seg[6 + 3 * c];
+                cp.h = seg[7 + 3 * c] >> 4;
+                cp.v = seg[7 + 3 * c] & 15;
+                cp.tq = seg[8 + 3 * c];
+                if (cp.h < 1 || cp.h > 4 || cp.v < 1 || cp.v > 4 || cp.tq > 3) return ACMMP_ERR_IO;
+                j.hmax = std::max(j.hmax, cp.h);
+                j.vmax = std::max(j.vmax, cp.v);
+            }
+            j.sof = true;
+            W = j.W;
+            H = j.H;
+            if (size_only) return ACMMP_OK;
+            // luminance = first component; it must carry the maximal sampling
+            // factors (libjpeg's grayscale output then needs no upsampling)
+            Comp &y = j.comp[0];
+            if (y.h != j.hmax || y.v != j.vmax) return ACMMP_ERR_UNSUPPORTED;
+            const int mcus_x = (j.W + 8 * j.hmax - 1) / (8 * j.hmax);
+            const int mcus_y = (j.H + 8 * j.vmax - 1) / (8 * j.vmax);
+            y.bw = mcus_x * y.h;
+            y.bh = mcus_y * y.v;
+            y.coef.assign((size_t)y.bw * y.bh * 64, 0);
+        } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+            return ACMMP_ERR_UNSUPPORTED;  // progressive, lossless, arithmetic
+        } else if (m == 0xDB) {  // DQT
+            int o = 0;
+            while (o < n) {
+                const int pq = seg[o] >> 4, tq = seg[o] & 15;
+                if (tq > 3 || o + 1 + 64 * (pq + 1) > n) return ACMMP_ERR_IO;
+                for (int k = 0; k < 64; ++k)
+                    j.qt[tq][kZigzag[k]] = pq ? (uint16_t)u16(seg + o + 1 + 2 * k) : seg[o + 1 + k];
+                j.qt_present[tq] = true;
+                o += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xC4) {  // DHT
+            int o = 0;
+            while (o < n) {
+                if (o + 17 > n) return ACMMP_ERR_IO;
+                const int tc = seg[o] >> 4, th = seg[o] & 15;
+                int total = 0;
+                for (int k = 0; k < 16; ++k) total += seg[o + 1 + k];
+                if (th > 3 || tc > 1 || o + 17 + total > n) return ACMMP_ERR_IO;
+                Huff &h = tc ? j.ac[th] : j.dc[th];
+                if (!build_huff(h, seg + o + 1, seg + o + 17, total)) return ACMMP_ERR_IO;
+                o += 17 + total;
+            }
+        } else if (m == 0xDD) {  // DRI
+            if (n < 2) return ACMMP_ERR_IO;
+            j.restart = u16(seg);
+        } else if (m == 0xDA) {  // SOS
+            if (!j.sof) return ACMMP_ERR_IO;
+            if (!decode_scan(j, seg, n)) return j.err ? j.err : ACMMP_ERR_UNSUPPORTED;
+            decoded = true;
+        }
+    }
+    if (!j.sof) return ACMMP_ERR_IO;
+    if (size_only) return ACMMP_OK;
+    if (!decoded || !j.qt_present[j.comp[0].tq]) return ACMMP_ERR_IO;
+    const Comp &y = j.comp[0];
+    const int pw = y.bw * 8, ph = y.bh * 8;
+    std::vector<uint8_t> full((size_t)pw * ph);
+    for (int by = 0; by < y.bh; ++by)
+        for (int bx = 0; bx < y.bw; ++bx)
+            idct_islow(&y.coef[((size_t)by * y.bw + bx) * 64], j.qt[y.tq], &full[(size_t)by * 8 * pw + bx * 8], pw);
+    gray->resize((size_t)j.W * j.H);
+    for (int r = 0; r < j.H; ++r) std::memcpy(gray->data() + (size_t)r * j.W, &full[(size_t)r * pw], j.W);
+    return ACMMP_OK;
+}
+
+// ------------------------------------------------------------- PGM / PFM
+bool next_token(const std::vector<uint8_t> &b, size_t &o, std::string &tok) {
+    tok.clear();
+    while (o < b.size()) {
+        if (b[o] == '#') {
+            while (o < b.size() && b[o] != '\n') ++o;
+        } else if (std::isspace(b[o])) {
+            ++o;
+        } else {
+            break;
+        }
+    }
+    while (o < b.size() && !std::isspace(b[o])) tok += (char)b[o++];
+    return !tok.empty();
+}
+
+int pnm_decode(const std::vector<uint8_t> &b, bool size_only, int &W, int &H, std::vector<float> *out) {
+    size_t o = 0;
+    std::string magic, tw, th, tm;
+    if (!next_token(b, o, magic) || !next_token(b, o, tw) || !next_token(b, o, th) || !next_token(b, o, tm))
+        return ACMMP_ERR_IO;
+    W = std::atoi(tw.c_str());
+    H = std::atoi(th.c_str());
+    if (W <= 0 || H <= 0) return ACMMP_ERR_IO;
+    if (size_only) return ACMMP_OK;
+    ++o;  // single whitespace after the header
+    const size_t P = (size_t)W * H;
+    out->resize(P);
+    if (magic == "P5") {
+        const int maxv = std::atoi(tm.c_str());
+        const int bps = maxv > 255 ? 2 : 1;
+        if (maxv <= 0 || maxv > 65535 || o + P * bps > b.size()) return ACMMP_ERR_IO;
+        for (size_t i = 0; i < P; ++i)
+            (*out)[i] = bps == 1 ? (float)b[o + i] : (float)((b[o + 2 * i] << 8) | b[o + 2 * i + 1]);
+        return ACMMP_OK;
+    }
+    if (magic == "Pf") {  // grayscale PFM: rows bottom-to-top, scale sign = endianness
+        const double scale = std::atof(tm.c_str());
+        if (o + P * 4 > b.size()) return ACMMP_ERR_IO;
+        const bool little = scale < 0;
+        for (int r = 0; r < H; ++r)
+            for (int c = 0; c < W; ++c) {
+                const uint8_t *q = &b[o + ((size_t)(H - 1 - r) * W + c) * 4];
+                uint32_t u = little ? (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24
+                                    : (uint32_t)q[3] | (uint32_t)q[2] << 8 | (uint32_t)q[1] << 16 | (uint32_t)q[0] << 24;
+                float f;
+                std::memcpy(&f, &u, 4);
+                (*out)[(size_t)r * W + c] = f;
+            }
+        return ACMMP_OK;
+    }
+    return ACMMP_ERR_UNSUPPORTED;
+}
+
+int decode_any(const char *path, bool size_only, int &W, int &H, std::vector<float> *out) {
+    std::vector<uint8_t> buf;
+    if (!path || !read_file(path, buf)) return ACMMP_ERR_IO;
+    if (buf.size() >= 2 && buf[0] == 0xFF && buf[1] == 0xD8) {
+        std::vector<uint8_t> g;
+        const int rc = jpeg_decode(buf, size_only, W, H, size_only ? nullptr : &g);
+        if (rc || size_only) return rc;
+        out->resize(g.size());
+        for (size_t i = 0; i < g.size(); ++i) (*out)[i] = (float)g[i];  // convertTo(CV_32FC1)
+        return ACMMP_OK;
+    }
+    if (buf.size() >= 2 && buf[0] == 'P') return pnm_decode(buf, size_only, W, H, out);
+    return ACMMP_ERR_UNSUPPORTED;
+}
+
+// ------------------------------------------------------------- resize
+// cv::resize(src, dst, Size(nw, nh), 0, 0, INTER_LINEAR) for CV_32FC1: the
+// exact-2x downscale takes OpenCV's INTER_AREA fast path (2x2 mean), other
+// factors the separable linear filter with half-pixel centres, edge clamp,
+// horizontal pass first.
+void resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh) {
+    const double sx = (double)sw / dw, sy = (double)sh / dh;
+    const int isx = (int)std::lround(sx), isy = (int)std::lround(sy);
+    if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16 && isx == 2 &&
+        isy == 2) {
+        for (int y = 0; y < dh; ++y)
+            for (int x = 0; x < dw; ++x) {
+                const float *r0 = src + (size_t)(2 * y) * sw + 2 * x, *r1 = r0 + sw;
+                dst[(size_t)y * dw + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+            }
+        return;
+    }
+    std::vector<int> x0(dw), x1(dw);
+    std::vector<float> ax(dw);
+    for (int x = 0; x < dw; ++x) {
+        float fx = (float)((x + 0.5) * sx - 0.5);
+        int ix = (int)std::floor(fx);
+        fx -= (float)ix;
+        if (ix < 0) {
+            fx = 0.f;
+            ix = 0;
+        }
+        if (ix >= sw - 1) {
+            fx = 0.f;
+            ix = sw - 1;
+        }
+        x0[x] = ix;
+        x1[x] = std::min(ix + 1, sw - 1);
+        ax[x] = fx;
+    }
+    std::vector<float> row0(dw), row1(dw);
+    for (int y = 0; y < dh; ++y) {
+        float fy = (float)((y + 0.5) * sy - 0.5);
+        int iy = (int)std::floor(fy);
+        fy -= (float)iy;
+        if (iy < 0) {
+            fy = 0.f;
+            iy = 0;
+        }
+        if (iy >= sh - 1) {
+            fy = 0.f;
+            iy = sh - 1;
+        }
+        const int iy1 = std::min(iy + 1, sh - 1);
+        const float *s0 = src + (size_t)iy * sw, *s1 = src + (size_t)iy1 * sw;
+        for (int x = 0; x < dw; ++x) {
+            row0[x] = s0[x0[x]] * (1.f - ax[x]) + s0[x1[x]] * ax[x];
+            row1[x] = s1[x0[x]] * (1.f - ax[x]) + s1[x1[x]] * ax[x];
+        }
+        for (int x = 0; x < dw; ++x) dst[(size_t)y * dw + x] = row0[x] * (1.f - fy) + row1[x] * fy;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int acmmp_image_size(const char *path, int *width, int *height) {
+    if (!width || !height) return ACMMP_ERR_ARG;
+    int W = 0, H = 0;
+    const int rc = decode_any(path, true, W, H, nullptr);
+    if (rc) return rc;
+    *width = W;
+    *height = H;
+    return ACMMP_OK;
+}
+
+int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *width, int *height) {
+    if (!width || !height) return ACMMP_ERR_ARG;
+    int W = 0, H = 0;
+    std::vector<float> img;
+    const int rc = decode_any(path, false, W, H, &img);
+    if (rc) return rc;
+    *width = W;
+    *height = H;
+    if (!out || capacity < img.size()) return ACMMP_ERR_ARG;
+    std::memcpy(out, img.data(), img.size() * sizeof(float));
+    return ACMMP_OK;
+}
+
+int acmmp_resize_linear(const float *src, int src_width, int src_height, float *dst, int dst_width,
+                        int dst_height) {
+    if (!src || !dst || src_width <= 0 || src_height <= 0 || dst_width <= 0 || dst_height <= 0) return ACMMP_ERR_ARG;
+    resize_linear(src, src_width, src_height, dst, dst_width, dst_height);
+    return ACMMP_OK;
+}
+
+}  // extern "C"

@@ -124,3 +124,45 @@ def write_pair(path: str, view_sel: list[list[tuple[int, float]]]) -> None:
 
 def result_folder(output_folder: str, ref_image_id: int) -> str:
     return os.path.join(output_folder, "2333_%08d" % ref_image_id)
+
+
+def read_image_gray(path: str) -> np.ndarray:
+    """cv::imread(path, IMREAD_GRAYSCALE) -> float32 (src/ACMMP.cpp:538-541)
+    through the library's decoder (baseline JPEG luminance / PGM / PFM)."""
+    import ctypes as C
+    lib = _abi.load_library()
+    w, h = C.c_int(0), C.c_int(0)
+    rc = lib.acmmp_image_size(path.encode(), C.byref(w), C.byref(h))
+    if rc != 0:
+        raise IOError(f"{path}: cannot read image header (status {rc})")
+    out = np.empty((h.value, w.value), dtype=np.float32)
+    rc = lib.acmmp_read_image_gray(path.encode(), out.ctypes.data_as(C.POINTER(C.c_float)), out.size,
+                                   C.byref(w), C.byref(h))
+    if rc != 0:
+        raise IOError(f"{path}: cannot decode image (status {rc})")
+    return out
+
+
+def image_size(path: str) -> tuple[int, int]:
+    """(width, height) from the file header."""
+    import ctypes as C
+    lib = _abi.load_library()
+    w, h = C.c_int(0), C.c_int(0)
+    rc = lib.acmmp_image_size(path.encode(), C.byref(w), C.byref(h))
+    if rc != 0:
+        raise IOError(f"{path}: cannot read image header (status {rc})")
+    return w.value, h.value
+
+
+def resize_linear(img: np.ndarray, width: int, height: int) -> np.ndarray:
+    """cv::resize(..., INTER_LINEAR) of a float image (src/ACMMP.cpp:589)."""
+    import ctypes as C
+    lib = _abi.load_library()
+    src = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.empty((height, width), dtype=np.float32)
+    fp = C.POINTER(C.c_float)
+    rc = lib.acmmp_resize_linear(src.ctypes.data_as(fp), src.shape[1], src.shape[0], out.ctypes.data_as(fp),
+                                 width, height)
+    if rc != 0:
+        raise ValueError(f"acmmp_resize_linear failed (status {rc})")
+    return out

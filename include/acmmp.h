@@ -255,6 +255,22 @@ const char *acmmp_version(void);
 /* ---- Reference on-disk formats (src/ACMMP.cpp:154-380,
  *      src/acmmp_definitions.cpp:179-205). Pure host code. ---- */
 
+/* ~ cv::imread(path, cv::IMREAD_GRAYSCALE) + convertTo(CV_32FC1) as used by
+ * InputInitialization (src/ACMMP.cpp:538-541, :553-556): baseline JPEG
+ * (luminance plane, libjpeg ISLOW IDCT), binary PGM (P5) or grayscale PFM.
+ * Writes width*height floats (row-major) when capacity suffices; otherwise
+ * returns ACMMP_ERR_ARG with *width / *height set. */
+int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *width, int *height);
+/* Image dimensions from the file header only (ComputeMultiScaleSettings,
+ * src/acmmp_definitions.cpp:219-224, decodes the whole image for this). */
+int acmmp_image_size(const char *path, int *width, int *height);
+/* ~ cv::resize(src, dst, Size(dst_width, dst_height), 0, 0, INTER_LINEAR) on
+ * a float image (src/ACMMP.cpp:589): half-pixel centres, edge clamp,
+ * horizontal pass first; an exact 2x downscale is the 2x2 mean (OpenCV's
+ * INTER_AREA fast path). */
+int acmmp_resize_linear(const float *src, int src_width, int src_height, float *dst, int dst_width,
+                        int dst_height);
+
 /* ReadCamera (src/ACMMP.cpp:154-179). width/height are left 0. */
 int acmmp_read_camera(const char *path, acmmp_camera *cam);
 /* readDepthDmb / readNormalDmb (src/ACMMP.cpp:264-294, :323-353): on success
