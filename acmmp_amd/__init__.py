@@ -7,7 +7,7 @@ on-disk formats (io), seeded synthetic scenes (scene) and the multi-view pass
 driver (driver).
 """
 from ._abi import Camera, Params, default_params, load_library  # noqa: F401
-from .engine import ACMMP, AcmmpError, make_camera, device_count, delaunay_triangulation  # noqa: F401
+from .engine import ACMMP, AcmmpError, make_camera, device_count, delaunay_triangulation, joint_bilateral_upsample  # noqa: F401
 
 __all__ = ["ACMMP", "AcmmpError", "Camera", "Params", "default_params", "load_library",
            "make_camera", "device_count"]

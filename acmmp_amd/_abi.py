@@ -135,6 +135,8 @@ SIGNATURES = {
                                                C.POINTER(C.c_int)]),
     "acmmp_build_planar_prior": (C.c_int, [_CTX, _I32P, C.c_int, _FP, _U32P]),
     "acmmp_prepare_planar_prior": (C.c_int, [_CTX, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "acmmp_joint_bilateral_upsample": (C.c_int, [C.c_int, _FP, C.c_int, C.c_int, _FP, C.c_int, C.c_int, _FP,
+                                                 C.POINTER(C.c_int)]),
     "acmmp_run_patchmatch": (C.c_int, [_CTX]),
     "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
     "acmmp_synchronize": (C.c_int, [_CTX]),

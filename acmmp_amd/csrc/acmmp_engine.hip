@@ -6,6 +6,7 @@
 // reports failures as status codes instead of exit().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -698,6 +699,36 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
     dfree(d_pl);
     dfree(d_out);
     return ACMMP_OK;
+}
+
+int acmmp_joint_bilateral_upsample(int device, const float *image, int width, int height, const float *depth,
+                                   int depth_width, int depth_height, float *out, int *image_scale) {
+    if (!image || !depth || !out || width <= 0 || height <= 0 || depth_width <= 0 || depth_height <= 0)
+        return ACMMP_ERR_ARG;
+    // RunJBU (src/ACMMP.cpp:1012-1021): Imagescale from integer size ratios;
+    // 1 means nothing to upsample and the reference writes nothing.
+    const int isc = std::max(height / depth_height, width / depth_width);
+    if (image_scale) *image_scale = isc;
+    if (isc <= 1) return ACMMP_OK;
+    if (isc > 64) return ACMMP_ERR_UNSUPPORTED;
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    const size_t P = (size_t)width * height, S = (size_t)depth_width * depth_height;
+    float *d_img = nullptr, *d_dep = nullptr, *d_out = nullptr;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc((void **)&d_img, P * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void **)&d_dep, S * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void **)&d_out, P * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpyAsync(d_img, image, P * sizeof(float), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_dep, depth, S * sizeof(float), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_jbu(d_img, width, height, d_dep, depth_width, depth_height, isc, d_out, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, P * sizeof(float), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (d_img) (void)hipFree(d_img);
+    if (d_dep) (void)hipFree(d_dep);
+    if (d_out) (void)hipFree(d_out);
+    if (s) (void)hipStreamDestroy(s);
+    return e == hipSuccess ? ACMMP_OK : ACMMP_ERR_HIP;
 }
 
 int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked) {

@@ -1395,7 +1395,51 @@ hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long 
     return hipGetLastError();
 }
 
+// JBU_cu (src/ACMMP.cu:1458-1516): joint-bilateral upsampling of a low-res
+// depth map guided by the high-res reference image; one thread per high-res
+// pixel. Texture reads at integer + 0.5 are exact texels (pin A4).
+__global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int W, int H,
+                                             const float *__restrict__ depth, int sw, int sh, int image_scale,
+                                             float *__restrict__ out) {
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y;
+    if (px >= W || py >= H) return;
+    const float scale = (float)(1.0 * sw / W);
+    const float sigmad = 0.50f, sigmar = 25.5f;
+    const int nn = (image_scale * image_scale + 1) / 2;
+    const float o_y = (float)py * scale;
+    const float o_x = (float)px * scale;
+    const float refPix = img[(size_t)py * W + px];
+    float total_val = 0.0f, normalizing_factor = 0.0f;
+    for (int j = -nn; j <= nn; ++j) {
+        int r_y = (int)(o_y + (float)j);
+        r_y = (r_y > 0 ? (r_y < sh ? r_y : sh - 1) : 0);
+        int r_ys = py + j;
+        r_ys = (r_ys > 0 ? (r_ys < H ? r_ys : H - 1) : 0);
+        for (int i = -nn; i <= nn; ++i) {
+            int r_x = (int)(o_x + (float)i);
+            r_x = (r_x > 0 ? (r_x < sw ? r_x : sw - 1) : 0);
+            const float srcPix = depth[(size_t)r_y * sw + r_x];
+            int r_xs = px + i;
+            r_xs = (r_xs > 0 ? (r_xs < W ? r_xs : W - 1) : 0);
+            const float nb = img[(size_t)r_ys * W + r_xs];
+            const float tg = spatial_gauss(o_x, o_y, (float)r_x, (float)r_y, sigmad) *
+                             range_gauss(dm_fabs(refPix - nb), sigmar);
+            normalizing_factor += tg;
+            total_val += srcPix * tg;
+        }
+    }
+    out[(size_t)py * W + px] = total_val / normalizing_factor;
+}
+
 // ---------------------------------------------------------------- launchers
+hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
+                      float *out, hipStream_t stream) {
+    dim3 block(64, 4), grid((W + 63) / 64, (H + 3) / 4);
+    k_jbu<<<grid, block, 0, stream>>>(img, W, H, depth, sw, sh, image_scale, out);
+    return hipGetLastError();
+}
+
 // Source-view count -> array capacity of the templated kernels.
 static int ns_bucket(int nsrc) {
     if (nsrc <= 4) return 4;

@@ -63,6 +63,22 @@ def delaunay_triangulation(width: int, height: int, points: np.ndarray) -> np.nd
     return tris[: n.value].copy()
 
 
+def joint_bilateral_upsample(image: np.ndarray, depth: np.ndarray, device: int = 0):
+    """RunJBU + JBU_cu (src/ACMMP.cpp:1008-1087, src/ACMMP.cu:1458-1549) on the
+    GPU. Returns (upsampled depth at the image's size, Imagescale); the depth
+    is None when Imagescale == 1 (the reference writes nothing then)."""
+    lib = _abi.load_library()
+    im = np.ascontiguousarray(image, dtype=np.float32)
+    d = np.ascontiguousarray(depth, dtype=np.float32)
+    out = np.empty_like(im)
+    isc = C.c_int(0)
+    rc = lib.acmmp_joint_bilateral_upsample(int(device), _fptr(im), im.shape[1], im.shape[0], _fptr(d), d.shape[1],
+                                            d.shape[0], _fptr(out), C.byref(isc))
+    if rc != 0:
+        raise AcmmpError(f"acmmp_joint_bilateral_upsample failed (status {rc})")
+    return (None if isc.value <= 1 else out), isc.value
+
+
 def device_count() -> int:
     return int(_abi.load_library().acmmp_device_count())
 

@@ -194,6 +194,15 @@ int acmmp_build_planar_prior(acmmp_ctx *ctx, const int32_t *tris, int num_triang
  * drawing. */
 int acmmp_prepare_planar_prior(acmmp_ctx *ctx, int *num_support_points, int *num_triangles);
 
+/* ~ RunJBU + JBU_cu (src/ACMMP.cpp:1008-1087, src/ACMMP.cu:1458-1549): joint
+ * bilateral upsampling of a low-res depth map (depth_width x depth_height)
+ * to the reference image's size (width x height, the image already resized
+ * to the current scale), on `device`. *image_scale receives
+ * max(height / depth_height, width / depth_width); when it is 1 nothing is
+ * computed or written, as in the reference. Host buffers in and out. */
+int acmmp_joint_bilateral_upsample(int device, const float *image, int width, int height, const float *depth,
+                                   int depth_width, int depth_height, float *out, int *image_scale);
+
 /* ~ ACMMP::RunPatchMatch (src/ACMMP.cu:1378-1456): init, max_iterations x
  * (black, red) checkerboard sweeps, depth/normal conversion, black/red median
  * filter. Results stay resident on the device; then rng_stream += 1. */

@@ -1290,3 +1290,45 @@ int acmmp_oracle_checkerboard_rows(int H) { return checkerboard_rows(H); }
 uint32_t acmmp_oracle_philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     return dm_philox_x(k0, k1, c0, c1, c2, c3);
 }
+
+/* JBU_cu (src/ACMMP.cu:1458-1516) with RunJBU's Imagescale
+ * (src/ACMMP.cpp:1014). Returns Imagescale; writes nothing when it is 1. */
+int acmmp_oracle_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, float *out) {
+    const int isc = (H / sh) > (W / sw) ? (H / sh) : (W / sw);
+    if (isc == 1) return isc;
+    const int WinWidth = isc * isc + 1;
+    const int num_neighbors = WinWidth / 2;
+    #pragma omp parallel for schedule(static)
+    for (int py = 0; py < H; ++py) {
+        for (int px = 0; px < W; ++px) {
+            const float scale = 1.0 * sw / W;
+            const float sigmad = 0.50;
+            const float sigmar = 25.5;
+            const float o_y = py * scale;
+            const float o_x = px * scale;
+            const float refPix = img[py * W + px];
+            float total_val = 0.0, normalizing_factor = 0.0;
+            for (int j = -num_neighbors; j <= num_neighbors; ++j) {
+                int r_y = o_y + j;
+                r_y = (r_y > 0 ? (r_y < sh ? r_y : sh - 1) : 0);
+                int r_ys = py + j;
+                r_ys = (r_ys > 0 ? (r_ys < H ? r_ys : H - 1) : 0);
+                for (int i = -num_neighbors; i <= num_neighbors; ++i) {
+                    int r_x = o_x + i;
+                    r_x = (r_x > 0 ? (r_x < sw ? r_x : sw - 1) : 0);
+                    const float srcPix = depth[r_y * sw + r_x];
+                    int r_xs = px + i;
+                    r_xs = (r_xs > 0 ? (r_xs < W ? r_xs : W - 1) : 0);
+                    const float neighborPix = img[r_ys * W + r_xs];
+                    const float sgauss = SpatialGauss(o_x, o_y, r_x, r_y, sigmad);
+                    const float rgauss = RangeGauss(fabsf(refPix - neighborPix), sigmar);
+                    const float totalgauss = sgauss * rgauss;
+                    normalizing_factor += totalgauss;
+                    total_val += srcPix * totalgauss;
+                }
+            }
+            out[py * W + px] = total_val / normalizing_factor;
+        }
+    }
+    return isc;
+}

@@ -68,6 +68,8 @@ def _load():
     lib.acmmp_oracle_planar_prior.restype = None
     lib.acmmp_oracle_planar_prior.argtypes = [CAM, FP, C.c_int, C.c_int, C.c_float, C.c_float, I32P, C.c_int,
                                               FP, U32P, FP]
+    lib.acmmp_oracle_jbu.restype = C.c_int
+    lib.acmmp_oracle_jbu.argtypes = [FP, C.c_int, C.c_int, FP, C.c_int, C.c_int, FP]
     _lib = lib
     return lib
 
@@ -220,3 +222,14 @@ def planar_prior(cam, depths, depth_min, depth_max, triangles):
     lib.acmmp_oracle_planar_prior(C.byref(cam), _f(d), w, h, float(depth_min), float(depth_max), _i(tr),
                                   int(tr.shape[0]), _f(planes), _u(mask), _f(prior))
     return planes[: tr.shape[0]], mask, prior
+
+
+def jbu(image, depth):
+    """JBU_cu / RunJBU (src/ACMMP.cu:1458-1516, src/ACMMP.cpp:1008-1087).
+    Returns (upsampled depth or None when Imagescale == 1, Imagescale)."""
+    lib = _load()
+    im = np.ascontiguousarray(image, dtype=np.float32)
+    d = np.ascontiguousarray(depth, dtype=np.float32)
+    out = np.zeros_like(im)
+    isc = lib.acmmp_oracle_jbu(_f(im), im.shape[1], im.shape[0], _f(d), d.shape[1], d.shape[0], _f(out))
+    return (None if isc == 1 else out), isc
