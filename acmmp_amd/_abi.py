@@ -102,6 +102,40 @@ def default_params() -> Params:
     return p
 
 
+class Problem(C.Structure):
+    """acmmp_problem == struct Problem (src/acmmp_definitions.h:57-63)."""
+    _fields_ = [
+        ("ref_image_id", C.c_int32),
+        ("num_src_images", C.c_int32),
+        ("src_image_ids", C.c_int32 * (MAX_IMAGES - 1)),
+        ("max_image_size", C.c_int32),
+        ("num_downscale", C.c_int32),
+        ("cur_image_size", C.c_int32),
+    ]
+
+    @property
+    def sources(self) -> list:
+        return list(self.src_image_ids[: self.num_src_images])
+
+
+class PassOptions(C.Structure):
+    """acmmp_pass_options: ProcessProblem's flags (src/acmmp_definitions.cpp:245-250)."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("geom_consistency", C.c_int32),
+        ("planar_prior", C.c_int32),
+        ("hierarchy", C.c_int32),
+        ("multi_geometry", C.c_int32),
+        ("seeded", C.c_int32),
+        ("max_iterations", C.c_int32),
+        ("seed_lo", C.c_uint32),
+        ("seed_hi", C.c_uint32),
+        ("write_triangulation", C.c_int32),
+        ("verbose", C.c_int32),
+        ("reserved", C.c_int32 * 5),
+    ]
+
+
 _FP = C.POINTER(C.c_float)
 _U32P = C.POINTER(C.c_uint32)
 _CTX = C.c_void_p
@@ -153,6 +187,17 @@ SIGNATURES = {
     "acmmp_selftest_reciprocal": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "acmmp_device_count": (C.c_int, []),
     "acmmp_version": (C.c_char_p, []),
+    "acmmp_generate_sample_list": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
+    "acmmp_compute_multiscale_settings": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
+    "acmmp_input_initialization": (C.c_int, [_CTX, C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int]),
+    "acmmp_space_initialization": (C.c_int, [_CTX, C.c_char_p, C.POINTER(Problem)]),
+    "acmmp_process_problem": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int,
+                                        C.POINTER(PassOptions)]),
+    "acmmp_joint_bilateral_upsampling": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int]),
+    "acmmp_pipeline_last_error": (C.c_char_p, []),
+    "acmmp_get_reference_image": (C.c_int, [_CTX, _FP, C.c_size_t]),
+    "acmmp_prior_plane_params": (C.c_int, [C.POINTER(Camera), _I32P, _FP, _FP]),
+    "acmmp_depth_from_plane_param": (C.c_float, [C.POINTER(Camera), _FP, C.c_int, C.c_int]),
     "acmmp_read_image_gray": (C.c_int, [C.c_char_p, _FP, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_image_size": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_resize_linear": (C.c_int, [_FP, C.c_int, C.c_int, _FP, C.c_int, C.c_int]),

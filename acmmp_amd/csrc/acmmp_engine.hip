@@ -639,6 +639,17 @@ int acmmp_get_reference_size(const acmmp_ctx *ctx, int *width, int *height) {
     return ACMMP_OK;
 }
 
+int acmmp_get_reference_image(acmmp_ctx *ctx, float *out, size_t n) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!out || n < (size_t)ctx->W * ctx->H) return set_err(ctx, ACMMP_ERR_ARG, "output capacity too small");
+    HIP_TRY(ctx, hipMemcpy2DAsync(out, (size_t)ctx->W * sizeof(float), ctx->img[0],
+                                  (size_t)ctx->img_pitch[0] * sizeof(float), (size_t)ctx->W * sizeof(float),
+                                  (size_t)ctx->H, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ACMMP_OK;
+}
+
 int acmmp_get_camera(const acmmp_ctx *ctx, int index, acmmp_camera *cam) {
     if (!ctx || !cam || index < 0 || index >= ctx->n) return ACMMP_ERR_ARG;
     *cam = ctx->cams[index];

@@ -1,0 +1,160 @@
+// acmmp_main — command-line pass driver with the options of the reference's
+// main_ACMMP (src/main_ACMMP.cpp:9-176): multi-scale loop, photometric +
+// planar-prior pass, two geometric-consistency passes per scale, JBU and the
+// hierarchy pass on finer scales. Views are processed in order within a pass
+// (the reference's Gauss-Seidel schedule). No GUI calls.
+//
+// Fusion (RunFusion / RunPriorAwareFusion) is not part of this build; the
+// fusion options are accepted so existing command lines keep working, and the
+// .dmb outputs are the reference's, for its fuse_data.
+#include <sys/stat.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.h"
+
+namespace {
+
+void usage() {
+    std::printf(
+        "usage: acmmp_main <dense_folder> [options]\n"
+        "  --output_dir NAME        output working directory name (default /ACMMP)\n"
+        "  -p, --prior              run from a provided prior (not supported)\n"
+        "  --device N               HIP device (default 0)\n"
+        "  --iterations N           PatchMatch iterations per run (default: the reference's 2)\n"
+        "  --seed N                 base RNG seed (default 1234)\n"
+        "  --no_triangulation       do not write triangulation.png\n"
+        "  --quiet                  no progress output\n"
+        "  fusion options accepted and ignored: -f/--fuse_thresh, --multi_fusion, --force_fusion,\n"
+        "  --num_consistent_thresh, --single_match_penalty, --mask_dir, --image_override\n");
+}
+
+int die(const char *what) {
+    std::fprintf(stderr, "acmmp_main: %s: %s\n", what, acmmp_pipeline_last_error());
+    return 1;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    std::string dense_folder, output_dir = "/ACMMP";
+    bool prior = false, quiet = false, triangulation = true;
+    int device = 0, iterations = 0;
+    unsigned seed = 1234;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto value = [&](void) -> std::string {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "acmmp_main: %s needs a value\n", a.c_str());
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "-h" || a == "--help") {
+            usage();
+            return 1;  // as the reference (src/main_ACMMP.cpp:58-61)
+        } else if (a == "-p" || a == "--prior") {
+            prior = true;
+        } else if (a == "--output_dir") {
+            output_dir = value();
+        } else if (a == "--device") {
+            device = std::atoi(value().c_str());
+        } else if (a == "--iterations") {
+            iterations = std::atoi(value().c_str());
+        } else if (a == "--seed") {
+            seed = (unsigned)std::strtoul(value().c_str(), nullptr, 10);
+        } else if (a == "--no_triangulation") {
+            triangulation = false;
+        } else if (a == "--quiet") {
+            quiet = true;
+        } else if (a == "-f" || a == "--fuse_thresh" || a == "--num_consistent_thresh" ||
+                   a == "--single_match_penalty" || a == "--mask_dir" || a == "--image_override") {
+            value();
+        } else if (a == "--multi_fusion") {
+            if (i + 1 < argc && argv[i + 1][0] != '-') ++i;
+        } else if (a == "--force_fusion") {
+        } else if (!a.empty() && a[0] != '-' && dense_folder.empty()) {
+            dense_folder = a;
+        } else {
+            std::fprintf(stderr, "acmmp_main: unknown option %s\n", a.c_str());
+            usage();
+            return 2;
+        }
+    }
+    if (dense_folder.empty()) {
+        usage();
+        return 2;
+    }
+    if (prior) {
+        std::fprintf(stderr, "acmmp_main: initialisation from a prior (-p) is not supported by this build\n");
+        return 1;
+    }
+
+    std::vector<acmmp_problem> problems(4096);
+    int num_images = 0;
+    if (acmmp_generate_sample_list(dense_folder.c_str(), problems.data(), (int)problems.size(), &num_images))
+        return die("GenerateSampleList");
+    problems.resize((size_t)num_images);
+    if (!quiet) std::printf("There are %d problems needed to be processed!\n", num_images);
+    int max_num_downscale = -1;
+    if (acmmp_compute_multiscale_settings(dense_folder.c_str(), problems.data(), num_images, &max_num_downscale))
+        return die("ComputeMultiScaleSettings");
+    const std::string output_folder = dense_folder + output_dir;
+    ::mkdir(output_folder.c_str(), 0777);
+
+    acmmp_pass_options opt;
+    std::memset(&opt, 0, sizeof(opt));
+    opt.device = device;
+    opt.max_iterations = iterations;
+    opt.write_triangulation = triangulation ? 1 : 0;
+    opt.verbose = quiet ? 0 : 1;
+    unsigned pass = 0;
+    auto run_pass = [&](bool geom, bool planar, bool hier, bool multi) -> bool {
+        opt.geom_consistency = geom;
+        opt.planar_prior = planar;
+        opt.hierarchy = hier;
+        opt.multi_geometry = multi;
+        opt.seed_hi = pass++;
+        for (int i = 0; i < num_images; ++i) {
+            opt.seed_lo = seed + (unsigned)problems[(size_t)i].ref_image_id;
+            if (acmmp_process_problem(dense_folder.c_str(), output_folder.c_str(), problems.data(), num_images, i,
+                                      &opt))
+                return false;
+        }
+        return true;
+    };
+
+    const int geom_iterations = 2;
+    int flag = 0;
+    while (max_num_downscale >= 0) {  // src/main_ACMMP.cpp:96-176
+        if (!quiet) std::printf("Scale: %d\n", max_num_downscale);
+        for (auto &p : problems) {
+            if (p.num_downscale >= 0) {
+                p.cur_image_size = (int)(p.max_image_size / std::pow(2, p.num_downscale));
+                p.num_downscale--;
+            }
+        }
+        if (flag == 0) {
+            flag = 1;
+            if (!run_pass(false, true, false, false)) return die("ProcessProblem");
+        } else {
+            if (!quiet) std::printf("Starting JBU\n");
+            for (auto &p : problems)
+                if (acmmp_joint_bilateral_upsampling(dense_folder.c_str(), output_folder.c_str(), &p,
+                                                     p.cur_image_size, device))
+                    return die("JointBilateralUpsampling");
+            if (!run_pass(false, true, true, false)) return die("ProcessProblem");
+        }
+        for (int g = 0; g < geom_iterations; ++g)
+            if (!run_pass(true, false, false, g > 0)) return die("ProcessProblem");
+        max_num_downscale--;
+    }
+    if (!quiet) std::printf("Depth/normal/cost maps written under %s (fusion not run by this build)\n",
+                            output_folder.c_str());
+    return 0;
+}

@@ -1,0 +1,455 @@
+// acmmp_pipeline.cpp — the reference's pass driver around RunPatchMatch, in
+// C++ over the library's own C-ABI (through include/acmmp.hpp):
+//
+//   GenerateSampleList          src/acmmp_definitions.cpp:179-205
+//   ComputeMultiScaleSettings   src/acmmp_definitions.cpp:207-243
+//   InputInitialization         src/ACMMP.cpp:525-636
+//   CudaSpaceInitialization     src/ACMMP.cpp:638-809 (previous-pass loading)
+//   ProcessProblem              src/acmmp_definitions.cpp:245-403
+//   JointBilateralUpsampling    src/acmmp_definitions.cpp:405-438 + RunJBU src/ACMMP.cpp:1008-1087
+//
+// File formats and names are the reference's, so an existing output folder,
+// fuse_data and later passes interoperate unchanged. Images are
+// `%08d.jpg` (decoded by acmmp_image.cpp); `%08d.pgm` / `%08d.pfm` are accepted
+// when no .jpg exists. Errors are status codes + acmmp_pipeline_last_error().
+#include <sys/stat.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+std::string id8(int id) {
+    char b[32];
+    std::snprintf(b, sizeof(b), "%08d", id);
+    return b;
+}
+
+bool exists(const std::string &p) {
+    struct stat st;
+    return ::stat(p.c_str(), &st) == 0;
+}
+
+std::string result_folder(const std::string &out, int ref_id) { return out + "/2333_" + id8(ref_id); }
+
+std::string image_path(const std::string &dense, int id) {
+    const std::string base = dense + "/images/" + id8(id);
+    for (const char *ext : {".jpg", ".pgm", ".pfm"})
+        if (exists(base + ext)) return base + ext;
+    return base + ".jpg";
+}
+
+int load_image(const std::string &path, acmmp::Image &im) {
+    int w = 0, h = 0;
+    int rc = acmmp_image_size(path.c_str(), &w, &h);
+    if (rc) return fail(rc, "cannot read image %s", path.c_str());
+    im.cols = w;
+    im.rows = h;
+    im.data.resize((size_t)w * h);
+    rc = acmmp_read_image_gray(path.c_str(), im.data.data(), im.data.size(), &w, &h);
+    if (rc) return fail(rc, "cannot decode image %s (baseline JPEG / PGM / PFM only)", path.c_str());
+    return ACMMP_OK;
+}
+
+int read_dmb(const std::string &path, std::vector<float> &data, int &h, int &w, int &nb) {
+    int32_t hh = 0, ww = 0, bb = 0;
+    int rc = acmmp_read_dmb(path.c_str(), &hh, &ww, &bb, nullptr, 0);
+    if (rc != ACMMP_OK && rc != ACMMP_ERR_ARG) return fail(ACMMP_ERR_IO, "cannot read %s", path.c_str());
+    data.resize((size_t)hh * ww * bb);
+    rc = acmmp_read_dmb(path.c_str(), &hh, &ww, &bb, data.data(), data.size());
+    if (rc) return fail(ACMMP_ERR_IO, "cannot read %s", path.c_str());
+    h = hh;
+    w = ww;
+    nb = bb;
+    return ACMMP_OK;
+}
+
+int write_dmb(const std::string &path, int h, int w, int nb, const float *data) {
+    if (acmmp_write_dmb(path.c_str(), h, w, nb, data)) return fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    return ACMMP_OK;
+}
+
+// ---- triangulation.png (src/acmmp_definitions.cpp:310-330): the reference
+// image as BGR with the triangle edges drawn in red, 1-px 8-connected lines.
+void put_chunk(std::vector<uint8_t> &png, const char *type, const std::vector<uint8_t> &data) {
+    const uint32_t n = (uint32_t)data.size();
+    const uint8_t len[4] = {(uint8_t)(n >> 24), (uint8_t)(n >> 16), (uint8_t)(n >> 8), (uint8_t)n};
+    png.insert(png.end(), len, len + 4);
+    const size_t start = png.size();
+    png.insert(png.end(), type, type + 4);
+    png.insert(png.end(), data.begin(), data.end());
+    const uLong crc = crc32(0L, png.data() + start, (uInt)(png.size() - start));
+    const uint8_t c[4] = {(uint8_t)(crc >> 24), (uint8_t)(crc >> 16), (uint8_t)(crc >> 8), (uint8_t)crc};
+    png.insert(png.end(), c, c + 4);
+}
+
+int write_png_rgb(const std::string &path, int w, int h, const std::vector<uint8_t> &rgb) {
+    std::vector<uint8_t> raw;
+    raw.reserve((size_t)h * (3 * w + 1));
+    for (int y = 0; y < h; ++y) {
+        raw.push_back(0);
+        raw.insert(raw.end(), rgb.begin() + (size_t)y * 3 * w, rgb.begin() + (size_t)(y + 1) * 3 * w);
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK)
+        return fail(ACMMP_ERR_IO, "zlib failed for %s", path.c_str());
+    z.resize(zlen);
+    std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::vector<uint8_t> ihdr = {(uint8_t)(w >> 24), (uint8_t)(w >> 16), (uint8_t)(w >> 8), (uint8_t)w,
+                                 (uint8_t)(h >> 24), (uint8_t)(h >> 16), (uint8_t)(h >> 8), (uint8_t)h,
+                                 8, 2, 0, 0, 0};
+    put_chunk(png, "IHDR", ihdr);
+    put_chunk(png, "IDAT", z);
+    put_chunk(png, "IEND", {});
+    FILE *f = std::fopen(path.c_str(), "wb");
+    if (!f) return fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    const bool ok = std::fwrite(png.data(), 1, png.size(), f) == png.size();
+    std::fclose(f);
+    return ok ? ACMMP_OK : fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+}
+
+void draw_line(std::vector<uint8_t> &rgb, int w, int h, acmmp::Point a, acmmp::Point b) {
+    int x0 = a.x, y0 = a.y;
+    const int dx = std::abs(b.x - x0), dy = -std::abs(b.y - y0);
+    const int sx = x0 < b.x ? 1 : -1, sy = y0 < b.y ? 1 : -1;
+    int e = dx + dy;
+    for (;;) {
+        if (x0 >= 0 && x0 < w && y0 >= 0 && y0 < h) {
+            uint8_t *p = &rgb[((size_t)y0 * w + x0) * 3];
+            p[0] = 255;
+            p[1] = 0;
+            p[2] = 0;
+        }
+        if (x0 == b.x && y0 == b.y) break;
+        const int e2 = 2 * e;
+        if (e2 >= dy) {
+            e += dy;
+            x0 += sx;
+        }
+        if (e2 <= dx) {
+            e += dx;
+            y0 += sy;
+        }
+    }
+}
+
+int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
+    const int W = acmmp.GetReferenceImageWidth(), H = acmmp.GetReferenceImageHeight();
+    const acmmp::Image ref = acmmp.GetReferenceImage();
+    std::vector<acmmp::Point> pts;
+    acmmp.GetSupportPoints(pts);
+    const auto tris = acmmp.DelaunayTriangulation(W, H, pts);
+    std::vector<uint8_t> rgb((size_t)W * H * 3);
+    for (size_t i = 0; i < (size_t)W * H; ++i) {
+        const float v = std::nearbyint(std::min(255.0f, std::max(0.0f, ref.data[i])));
+        rgb[3 * i] = rgb[3 * i + 1] = rgb[3 * i + 2] = (uint8_t)v;
+    }
+    for (const auto &t : tris) {
+        draw_line(rgb, W, H, t.pt1, t.pt2);
+        draw_line(rgb, W, H, t.pt1, t.pt3);
+        draw_line(rgb, W, H, t.pt2, t.pt3);
+    }
+    return write_png_rgb(path, W, H, rgb);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *acmmp_pipeline_last_error(void) { return g_err.c_str(); }
+
+int acmmp_generate_sample_list(const char *dense_folder, acmmp_problem *problems, int capacity, int *count) {
+    if (!dense_folder || !count || capacity < 0 || (capacity > 0 && !problems)) return fail(ACMMP_ERR_ARG, "bad args");
+    const std::string path = std::string(dense_folder) + "/pair.txt";
+    std::ifstream file(path);
+    if (!file.is_open()) return fail(ACMMP_ERR_IO, "cannot open %s", path.c_str());
+    int num_images = 0;
+    file >> num_images;
+    if (file.fail() || num_images < 0) return fail(ACMMP_ERR_IO, "bad header in %s", path.c_str());
+    *count = num_images;
+    if (num_images > capacity) return fail(ACMMP_ERR_ARG, "%d problems exceed capacity %d", num_images, capacity);
+    for (int i = 0; i < num_images; ++i) {
+        acmmp_problem pr;
+        std::memset(&pr, 0, sizeof(pr));
+        pr.max_image_size = 6400;  // struct Problem defaults (src/acmmp_definitions.h:57-63)
+        pr.cur_image_size = 6400;
+        int num_src = 0;
+        file >> pr.ref_image_id >> num_src;
+        for (int j = 0; j < num_src; ++j) {
+            int id;
+            float score;
+            file >> id >> score;
+            if (score <= 0.0f) continue;
+            if (pr.num_src_images == ACMMP_MAX_IMAGES - 1)
+                return fail(ACMMP_ERR_UNSUPPORTED, "view %d: more than %d sources", pr.ref_image_id,
+                            ACMMP_MAX_IMAGES - 1);
+            pr.src_image_ids[pr.num_src_images++] = id;
+        }
+        if (file.fail()) return fail(ACMMP_ERR_IO, "truncated %s", path.c_str());
+        problems[i] = pr;
+    }
+    return ACMMP_OK;
+}
+
+int acmmp_compute_multiscale_settings(const char *dense_folder, acmmp_problem *problems, int count,
+                                      int *max_num_downscale) {
+    if (!dense_folder || !problems || count < 0 || !max_num_downscale) return fail(ACMMP_ERR_ARG, "bad args");
+    acmmp_params pmp;
+    acmmp_default_params(&pmp);
+    const int size_bound = 1000;
+    int best = -1;
+    for (int i = 0; i < count; ++i) {
+        const std::string path = image_path(dense_folder, problems[i].ref_image_id);
+        int cols = 0, rows = 0;
+        const int rc = acmmp_image_size(path.c_str(), &cols, &rows);
+        if (rc) return fail(rc, "cannot read image %s", path.c_str());
+        int max_size = std::max(rows, cols);
+        if (max_size > pmp.max_image_size) max_size = pmp.max_image_size;
+        problems[i].max_image_size = max_size;
+        int k = 0;
+        while (max_size > size_bound) {
+            max_size /= 2;
+            k++;
+        }
+        best = std::max(best, k);
+        problems[i].num_downscale = k;
+    }
+    *max_num_downscale = best;
+    return ACMMP_OK;
+}
+
+int acmmp_input_initialization(acmmp_ctx *ctx, const char *dense_folder, const char *output_folder,
+                               const acmmp_problem *problems, int count, int idx) {
+    if (!ctx || !dense_folder || !output_folder || !problems || idx < 0 || idx >= count)
+        return fail(ACMMP_ERR_ARG, "bad args");
+    const acmmp_problem &pr = problems[idx];
+    const std::string dense = dense_folder;
+    const int n = 1 + pr.num_src_images;
+    if (n < 2 || n > ACMMP_MAX_IMAGES) return fail(ACMMP_ERR_ARG, "view %d has %d sources", pr.ref_image_id, n - 1);
+    std::vector<acmmp::Image> images((size_t)n);
+    std::vector<acmmp_camera> cams((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
+        int rc = load_image(image_path(dense, id), images[(size_t)i]);
+        if (rc) return rc;
+        const std::string cam_path = dense + "/cams/" + id8(id) + "_cam.txt";
+        rc = acmmp_read_camera(cam_path.c_str(), &cams[(size_t)i]);
+        if (rc) return fail(rc, "cannot read camera %s", cam_path.c_str());
+        cams[(size_t)i].height = images[(size_t)i].rows;
+        cams[(size_t)i].width = images[(size_t)i].cols;
+    }
+    // Scale cameras and images (src/ACMMP.cpp:564-598); a source view uses the
+    // cur_image_size of the problem indexed by its image id, as the reference does.
+    for (int i = 0; i < n; ++i) {
+        int max_image_size = pr.cur_image_size;
+        if (i > 0) {
+            const int sid = pr.src_image_ids[i - 1];
+            if (sid < 0 || sid >= count)
+                return fail(ACMMP_ERR_ARG, "source id %d is not a problem index (pair.txt ids must be 0..n-1)", sid);
+            max_image_size = problems[sid].cur_image_size;
+        }
+        acmmp::Image &im = images[(size_t)i];
+        if (im.cols <= max_image_size && im.rows <= max_image_size) continue;
+        const float factor_x = static_cast<float>(max_image_size) / im.cols;
+        const float factor_y = static_cast<float>(max_image_size) / im.rows;
+        const float factor = std::min(factor_x, factor_y);
+        const int new_cols = (int)std::round(im.cols * factor);
+        const int new_rows = (int)std::round(im.rows * factor);
+        const float scale_x = new_cols / static_cast<float>(im.cols);
+        const float scale_y = new_rows / static_cast<float>(im.rows);
+        acmmp::Image scaled;
+        scaled.cols = new_cols;
+        scaled.rows = new_rows;
+        scaled.data.resize((size_t)new_cols * new_rows);
+        acmmp_resize_linear(im.data.data(), im.cols, im.rows, scaled.data.data(), new_cols, new_rows);
+        im = std::move(scaled);
+        cams[(size_t)i].K[0] *= scale_x;
+        cams[(size_t)i].K[2] *= scale_x;
+        cams[(size_t)i].K[4] *= scale_y;
+        cams[(size_t)i].K[5] *= scale_y;
+        cams[(size_t)i].height = new_rows;
+        cams[(size_t)i].width = new_cols;
+    }
+    std::vector<const float *> ptrs((size_t)n);
+    for (int i = 0; i < n; ++i) ptrs[(size_t)i] = images[(size_t)i].data.data();
+    int rc = acmmp_set_images(ctx, n, cams.data(), ptrs.data(), 0);  // depth range x0.6 / x1.2 (:600-605)
+    if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
+    acmmp_params p;
+    acmmp_get_params(ctx, &p);
+    if (p.geom_consistency) {  // :608-635
+        const std::string suffix = p.multi_geometry ? "/depths_geom.dmb" : "/depths.dmb";
+        std::vector<std::vector<float>> depths((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
+            int h = 0, w = 0, nb = 0;
+            rc = read_dmb(result_folder(output_folder, id) + suffix, depths[(size_t)i], h, w, nb);
+            if (rc) return rc;
+            if (nb != 1 || h != cams[(size_t)i].height || w != cams[(size_t)i].width)
+                return fail(ACMMP_ERR_IO, "depth map of view %d is %dx%dx%d, image is %dx%d", id, w, h, nb,
+                            cams[(size_t)i].width, cams[(size_t)i].height);
+            ptrs[(size_t)i] = depths[(size_t)i].data();
+        }
+        rc = acmmp_set_depth_maps(ctx, ptrs.data());
+        if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
+    }
+    return ACMMP_OK;
+}
+
+int acmmp_space_initialization(acmmp_ctx *ctx, const char *output_folder, const acmmp_problem *problem) {
+    if (!ctx || !output_folder || !problem) return fail(ACMMP_ERR_ARG, "bad args");
+    acmmp_params p;
+    acmmp_get_params(ctx, &p);
+    int W = 0, H = 0;
+    acmmp_get_reference_size(ctx, &W, &H);
+    const std::string folder = result_folder(output_folder, problem->ref_image_id);
+    if (p.geom_consistency) {  // src/ACMMP.cpp:707-742
+        const std::string suffix = p.multi_geometry ? "/depths_geom.dmb" : "/depths.dmb";
+        std::vector<float> d, nrm, c;
+        int h = 0, w = 0, nb = 0, h2 = 0, w2 = 0, nb2 = 0, h3 = 0, w3 = 0, nb3 = 0;
+        int rc = read_dmb(folder + suffix, d, h, w, nb);
+        if (!rc) rc = read_dmb(folder + "/normals.dmb", nrm, h2, w2, nb2);
+        if (!rc) rc = read_dmb(folder + "/costs.dmb", c, h3, w3, nb3);
+        if (rc) return rc;
+        if (h != H || w != W || h2 != H || w2 != W || nb2 != 3 || h3 != H || w3 != W)
+            return fail(ACMMP_ERR_IO, "previous-pass maps of view %d do not match %dx%d", problem->ref_image_id, W, H);
+        std::vector<float> planes((size_t)W * H * 4);
+        for (size_t i = 0; i < (size_t)W * H; ++i) {
+            planes[4 * i] = nrm[3 * i];
+            planes[4 * i + 1] = nrm[3 * i + 1];
+            planes[4 * i + 2] = nrm[3 * i + 2];
+            planes[4 * i + 3] = d[i];
+        }
+        rc = acmmp_set_plane_hypotheses(ctx, planes.data(), c.data());
+        if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
+    }
+    if (p.hierarchy) {  // :745-808
+        std::vector<float> d, nrm, c;
+        int h = 0, w = 0, nb = 0, sh = 0, sw = 0, nb2 = 0, h3 = 0, w3 = 0, nb3 = 0;
+        int rc = read_dmb(folder + "/depths.dmb", d, h, w, nb);
+        if (!rc) rc = read_dmb(folder + "/normals.dmb", nrm, sh, sw, nb2);
+        if (!rc) rc = read_dmb(folder + "/costs.dmb", c, h3, w3, nb3);
+        if (rc) return rc;
+        if (h != H || w != W)
+            return fail(ACMMP_ERR_IO, "upsampled depth of view %d is %dx%d, image is %dx%d (run JBU first)",
+                        problem->ref_image_id, w, h, W, H);
+        if (nb2 != 3 || h3 != sh || w3 != sw) return fail(ACMMP_ERR_IO, "normals/costs of view %d disagree", problem->ref_image_id);
+        // the upsample test with the reference's rows/cols swap (:766)
+        const bool upsample = (sw != H || sh != W);
+        std::vector<float> scaled((size_t)sw * sh * 4);
+        for (size_t i = 0; i < (size_t)sw * sh; ++i) {
+            scaled[4 * i] = nrm[3 * i];
+            scaled[4 * i + 1] = nrm[3 * i + 1];
+            scaled[4 * i + 2] = nrm[3 * i + 2];
+            scaled[4 * i + 3] = upsample ? c[i] : (i < d.size() ? d[i] : 0.0f);
+        }
+        rc = acmmp_set_hierarchy_inputs(ctx, scaled.data(), sw, sh, d.data());
+        if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
+    }
+    return ACMMP_OK;
+}
+
+int acmmp_process_problem(const char *dense_folder, const char *output_folder, const acmmp_problem *problems,
+                          int count, int idx, const acmmp_pass_options *opt) {
+    if (!dense_folder || !output_folder || !problems || !opt || idx < 0 || idx >= count)
+        return fail(ACMMP_ERR_ARG, "bad args");
+    if (opt->seeded) return fail(ACMMP_ERR_UNSUPPORTED, "seeded priors (pSampler) are not supported");
+    const acmmp_problem &problem = problems[idx];
+    if (opt->verbose) std::printf("Processing image %s...\n", id8(problem.ref_image_id).c_str());
+    const std::string folder = result_folder(output_folder, problem.ref_image_id);
+    ::mkdir(folder.c_str(), 0777);
+    try {
+        acmmp::ACMMP acmmp(opt->device);
+        if (opt->geom_consistency) acmmp.SetGeomConsistencyParams(opt->multi_geometry != 0);
+        if (opt->hierarchy) acmmp.SetHierarchyParams();
+        acmmp_params p = acmmp.params();
+        p.seed_lo = opt->seed_lo;
+        p.seed_hi = opt->seed_hi;
+        if (opt->max_iterations > 0) p.max_iterations = opt->max_iterations;
+        acmmp.set_params(p);
+        std::vector<acmmp::Problem> all(problems, problems + count);
+        acmmp.InputInitialization(dense_folder, output_folder, all, idx);
+        acmmp.CudaSpaceInitialization(output_folder, problem);
+        const int width = acmmp.GetReferenceImageWidth(), height = acmmp.GetReferenceImageHeight();
+        acmmp.RunPatchMatch();
+        if (opt->planar_prior) {  // :301-379
+            if (opt->verbose) std::printf("Run Planar Prior Assisted PatchMatch MVS ...\n");
+            if (opt->write_triangulation) {
+                const int rc = write_triangulation(acmmp, folder + "/triangulation.png");
+                if (rc) return rc;
+            }
+            acmmp.PreparePlanarPrior();  // support points, Delaunay, prior planes; SetPlanarPriorParams
+            acmmp.RunPatchMatch();
+        }
+        const auto &planes = acmmp.GetPlaneHypotheses();
+        const auto &costs = acmmp.GetCosts();
+        const size_t P = (size_t)width * height;
+        std::vector<float> depths(P), normals(P * 3);
+        for (size_t i = 0; i < P; ++i) {
+            depths[i] = planes[i].w;
+            normals[3 * i] = planes[i].x;
+            normals[3 * i + 1] = planes[i].y;
+            normals[3 * i + 2] = planes[i].z;
+        }
+        const std::string suffix = opt->geom_consistency ? "/depths_geom.dmb" : "/depths.dmb";
+        int rc = write_dmb(folder + suffix, height, width, 1, depths.data());
+        if (!rc) rc = write_dmb(folder + "/normals.dmb", height, width, 3, normals.data());
+        if (!rc) rc = write_dmb(folder + "/costs.dmb", height, width, 1, costs.data());
+        if (rc) return rc;
+    } catch (const acmmp::Error &e) {
+        return fail(e.status(), "view %d: %s", problem.ref_image_id, e.what());
+    }
+    if (opt->verbose) std::printf("Processing image %s done!\n", id8(problem.ref_image_id).c_str());
+    return ACMMP_OK;
+}
+
+int acmmp_joint_bilateral_upsampling(const char *dense_folder, const char *output_folder,
+                                     const acmmp_problem *problem, int acmmp_size, int device) {
+    if (!dense_folder || !output_folder || !problem || acmmp_size <= 0) return fail(ACMMP_ERR_ARG, "bad args");
+    const std::string folder = result_folder(output_folder, problem->ref_image_id);
+    std::vector<float> depth;
+    int dh = 0, dw = 0, nb = 0;
+    int rc = read_dmb(folder + "/depths_geom.dmb", depth, dh, dw, nb);
+    if (rc) return rc;
+    acmmp::Image im;
+    rc = load_image(image_path(dense_folder, problem->ref_image_id), im);
+    if (rc) return rc;
+    const float factor_x = static_cast<float>(acmmp_size) / im.cols;
+    const float factor_y = static_cast<float>(acmmp_size) / im.rows;
+    const float factor = std::min(factor_x, factor_y);
+    const int new_cols = (int)std::round(im.cols * factor);
+    const int new_rows = (int)std::round(im.rows * factor);
+    std::vector<float> scaled((size_t)new_cols * new_rows);
+    acmmp_resize_linear(im.data.data(), im.cols, im.rows, scaled.data(), new_cols, new_rows);
+    std::vector<float> out(scaled.size());
+    int isc = 0;
+    rc = acmmp_joint_bilateral_upsample(device, scaled.data(), new_cols, new_rows, depth.data(), dw, dh, out.data(),
+                                        &isc);
+    if (rc) return fail(rc, "JBU of view %d failed", problem->ref_image_id);
+    if (isc <= 1) return ACMMP_OK;  // "Image.rows = Depthmap.rows": nothing written (src/ACMMP.cpp:1016-1019)
+    ::mkdir(folder.c_str(), 0777);
+    return write_dmb(folder + "/depths.dmb", new_rows, new_cols, 1, out.data());
+}
+
+}  // extern "C"

@@ -58,15 +58,13 @@ __global__ void k_support_points(const float *__restrict__ cost, int W, int H, i
     out[b] = (min_cost < 0.1f) ? (py << 16) | px : -1;
 }
 
-// GetPriorPlaneParams (src/ACMMP.cpp:920-953), one thread per triangle.
-__global__ void k_prior_planes(const float4 *__restrict__ rm_plane, int W, acmmp_camera cam,
-                               const int32_t *__restrict__ tris, int ntris, float4 *__restrict__ planes) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntris) return;
+// GetPriorPlaneParams (src/ACMMP.cpp:920-953) for triangle corners (x, y)
+// with depths d: host (acmmp_prior_plane_params) and device (k_prior_planes).
+__host__ __device__ inline float4 prior_plane(const acmmp_camera &cam, const int32_t *tri, const float *dk) {
     double A[3][4];
     for (int k = 0; k < 3; ++k) {
-        const int x = tris[6 * t + 2 * k], y = tris[6 * t + 2 * k + 1];
-        const float d = rm_plane[(size_t)y * W + x].w;  // depths(y, x) = plane.w after RunPatchMatch
+        const int x = tri[2 * k], y = tri[2 * k + 1];
+        const float d = dk[k];
         // Get3DPointonRefCam (src/ACMMP.cpp:230-239)
         const float X = d * ((float)x - cam.K[2]) / cam.K[0];
         const float Y = d * ((float)y - cam.K[5]) / cam.K[4];
@@ -78,9 +76,9 @@ __global__ void k_prior_planes(const float4 *__restrict__ rm_plane, int W, acmmp
     // null vector of A: n_j = (-1)^j det(A without column j)
     double n[4];
     for (int j = 0; j < 4; ++j) {
-        int c0 = j == 0 ? 1 : 0;
-        int c1 = j <= 1 ? 2 : 1;
-        int c2 = j <= 2 ? 3 : 2;
+        const int c0 = j == 0 ? 1 : 0;
+        const int c1 = j <= 1 ? 2 : 1;
+        const int c2 = j <= 2 ? 3 : 2;
         const double m =
             A[0][c0] * (A[1][c1] * A[2][c2] - A[1][c2] * A[2][c1]) -
             A[0][c1] * (A[1][c0] * A[2][c2] - A[1][c2] * A[2][c0]) +
@@ -96,7 +94,25 @@ __global__ void k_prior_planes(const float4 *__restrict__ rm_plane, int W, acmmp
     n4.y /= norm2;
     n4.z /= norm2;
     n4.w /= norm2;
-    planes[t] = n4;
+    return n4;
+}
+
+// GetDepthFromPlaneParam (src/ACMMP.cpp:955-958).
+__host__ __device__ inline float depth_from_plane(const acmmp_camera &cam, float4 pl, int x, int y) {
+    const float num = -pl.w * cam.K[0];
+    const float den =
+        ((float)x - cam.K[2]) * pl.x + (cam.K[0] / cam.K[4]) * ((float)y - cam.K[5]) * pl.y + cam.K[0] * pl.z;
+    return num / den;
+}
+
+__global__ void k_prior_planes(const float4 *__restrict__ rm_plane, int W, acmmp_camera cam,
+                               const int32_t *__restrict__ tris, int ntris, float4 *__restrict__ planes) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntris) return;
+    const int32_t *tri = tris + 6 * t;
+    float d[3];
+    for (int k = 0; k < 3; ++k) d[k] = rm_plane[(size_t)tri[2 * k + 1] * W + tri[2 * k]].w;  // depths(y, x)
+    planes[t] = prior_plane(cam, tri, d);
 }
 
 __device__ __forceinline__ float edge_len(int ax, int ay, int bx, int by) {
@@ -165,10 +181,7 @@ __global__ void k_prior_range(const float4 *__restrict__ planes, acmmp_camera ca
     float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
     if (l > 0) {
         pl = planes[l - 1];
-        const float num = -pl.w * cam.K[0];
-        const float den = ((float)x - cam.K[2]) * pl.x + (cam.K[0] / cam.K[4]) * ((float)y - cam.K[5]) * pl.y +
-                          cam.K[0] * pl.z;
-        const float d = num / den;
+        const float d = depth_from_plane(cam, pl, x, y);
         if (!(d <= dmax && d >= dmin)) {
             l = 0;
             label[i] = 0;
@@ -273,6 +286,21 @@ struct Delaunay {
 }  // namespace
 
 extern "C" {
+
+int acmmp_prior_plane_params(const acmmp_camera *cam, const int32_t *tri, const float *depths, float *out4) {
+    if (!cam || !tri || !depths || !out4) return ACMMP_ERR_ARG;
+    const float4 n4 = prior_plane(*cam, tri, depths);
+    out4[0] = n4.x;
+    out4[1] = n4.y;
+    out4[2] = n4.z;
+    out4[3] = n4.w;
+    return ACMMP_OK;
+}
+
+float acmmp_depth_from_plane_param(const acmmp_camera *cam, const float *plane4, int x, int y) {
+    if (!cam || !plane4) return 0.0f;
+    return depth_from_plane(*cam, make_float4(plane4[0], plane4[1], plane4[2], plane4[3]), x, y);
+}
 
 int acmmp_delaunay_triangulation(int width, int height, const int32_t *xy, int npoints, int32_t *tris,
                                  int capacity, int *ntris) {

@@ -1,0 +1,134 @@
+"""The reference's pass driver (src/main_ACMMP.cpp:96-176,
+src/acmmp_definitions.cpp:179-438) over the library's C-ABI.
+
+`run_sequential` is the single-process schedule of main_ACMMP: views in order
+inside a pass, so a second geometric pass reads maps already rewritten in the
+same pass (Gauss-Seidel). The same loop ships as the C++ command-line tool
+`acmmp_amd/lib/acmmp_main`; this module drives it in-process and is the base of
+the view-parallel driver (acmmp_amd/distributed.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Sequence
+
+from . import _abi
+from .engine import AcmmpError
+
+MAX_PROBLEMS = 1 << 14
+
+
+def _err(what: str, rc: int):
+    lib = _abi.load_library()
+    msg = lib.acmmp_pipeline_last_error().decode(errors="replace")
+    raise AcmmpError(f"{what} failed (status {rc}): {msg}")
+
+
+def generate_sample_list(dense_folder: str) -> list:
+    """GenerateSampleList (src/acmmp_definitions.cpp:179-205)."""
+    lib = _abi.load_library()
+    buf = (_abi.Problem * MAX_PROBLEMS)()
+    n = C.c_int(0)
+    rc = lib.acmmp_generate_sample_list(dense_folder.encode(), buf, MAX_PROBLEMS, C.byref(n))
+    if rc != 0:
+        _err("GenerateSampleList", rc)
+    return [buf[i] for i in range(n.value)]
+
+
+def _array(problems: Sequence):
+    arr = (_abi.Problem * len(problems))()
+    for i, p in enumerate(problems):
+        arr[i] = p
+    return arr
+
+
+def compute_multiscale_settings(dense_folder: str, problems: list) -> int:
+    """ComputeMultiScaleSettings (src/acmmp_definitions.cpp:207-243); updates
+    `problems` in place, returns max_num_downscale."""
+    lib = _abi.load_library()
+    arr = _array(problems)
+    k = C.c_int(-1)
+    rc = lib.acmmp_compute_multiscale_settings(dense_folder.encode(), arr, len(problems), C.byref(k))
+    if rc != 0:
+        _err("ComputeMultiScaleSettings", rc)
+    problems[:] = [arr[i] for i in range(len(problems))]
+    return k.value
+
+
+def pass_options(geom_consistency=False, planar_prior=False, hierarchy=False, multi_geometry=False,
+                 device=0, max_iterations=0, seed_lo=1234, seed_hi=0, write_triangulation=True,
+                 verbose=False) -> _abi.PassOptions:
+    o = _abi.PassOptions()
+    o.device = device
+    o.geom_consistency = int(geom_consistency)
+    o.planar_prior = int(planar_prior)
+    o.hierarchy = int(hierarchy)
+    o.multi_geometry = int(multi_geometry)
+    o.max_iterations = max_iterations
+    o.seed_lo = seed_lo & 0xFFFFFFFF
+    o.seed_hi = seed_hi & 0xFFFFFFFF
+    o.write_triangulation = int(write_triangulation)
+    o.verbose = int(verbose)
+    return o
+
+
+def process_problem(dense_folder: str, output_folder: str, problems: Sequence, idx: int,
+                    options: _abi.PassOptions) -> None:
+    """ProcessProblem (src/acmmp_definitions.cpp:245-403)."""
+    lib = _abi.load_library()
+    rc = lib.acmmp_process_problem(dense_folder.encode(), output_folder.encode(), _array(problems), len(problems),
+                                   idx, C.byref(options))
+    if rc != 0:
+        _err("ProcessProblem", rc)
+
+
+def joint_bilateral_upsampling(dense_folder: str, output_folder: str, problem, acmmp_size: int,
+                               device: int = 0) -> None:
+    """JointBilateralUpsampling (src/acmmp_definitions.cpp:405-438)."""
+    lib = _abi.load_library()
+    rc = lib.acmmp_joint_bilateral_upsampling(dense_folder.encode(), output_folder.encode(), C.byref(problem),
+                                              acmmp_size, device)
+    if rc != 0:
+        _err("JointBilateralUpsampling", rc)
+
+
+def scale_step(problems: list) -> None:
+    """cur_image_size for the next scale (src/main_ACMMP.cpp:99-106)."""
+    for p in problems:
+        if p.num_downscale >= 0:
+            p.cur_image_size = int(p.max_image_size / (2.0 ** p.num_downscale))
+            p.num_downscale -= 1
+
+
+def run_sequential(dense_folder: str, output_dir: str = "/ACMMP", device: int = 0, max_iterations: int = 0,
+                   seed: int = 1234, write_triangulation: bool = True, geom_iterations: int = 2,
+                   verbose: bool = False) -> str:
+    """main_ACMMP's multi-scale loop without fusion; returns the output folder."""
+    problems = generate_sample_list(dense_folder)
+    max_num_downscale = compute_multiscale_settings(dense_folder, problems)
+    output_folder = dense_folder + output_dir
+    os.makedirs(output_folder, exist_ok=True)
+    state = {"pass": 0}
+
+    def run_pass(geom, planar, hier, multi):
+        for i, p in enumerate(problems):
+            opt = pass_options(geom, planar, hier, multi, device, max_iterations, seed + p.ref_image_id,
+                               state["pass"], write_triangulation, verbose)
+            process_problem(dense_folder, output_folder, problems, i, opt)
+        state["pass"] += 1
+
+    first = True
+    while max_num_downscale >= 0:
+        scale_step(problems)
+        if first:
+            first = False
+            run_pass(False, True, False, False)
+        else:
+            for p in problems:
+                joint_bilateral_upsampling(dense_folder, output_folder, p, p.cur_image_size, device)
+            run_pass(False, True, True, False)
+        for g in range(geom_iterations):
+            run_pass(True, False, False, g > 0)
+        max_num_downscale -= 1
+    return output_folder

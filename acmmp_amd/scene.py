@@ -250,3 +250,32 @@ def make_scene(num_views: int = 10, width: int = 1600, height: int = 1200, seed:
     """Render `num_views` views on an arc (arc_deg apart) at width x height."""
     setup = scene_setup(num_views, width, height, seed, arc_deg, radius)
     return Scene(views=[render_numpy(setup, i) for i in range(num_views)], pairs=setup.pairs)
+
+
+def write_dense_folder(scene: Scene, folder: str, fmt: str = "jpg", quality: int = 95,
+                       num_src: int | None = None) -> None:
+    """A COLMAP-converted dense folder (images/%08d.jpg, cams/%08d_cam.txt,
+    pair.txt) as colmap2mvsnet_acm.py writes it (:426-445), for the scene's
+    views. The depth line is DEPTH_LINE."""
+    import os
+    from . import io as _io
+    os.makedirs(os.path.join(folder, "images"), exist_ok=True)
+    os.makedirs(os.path.join(folder, "cams"), exist_ok=True)
+    for i, v in enumerate(scene.views):
+        img = np.clip(np.rint(v.image), 0, 255).astype(np.uint8)
+        path = os.path.join(folder, "images", "%08d.%s" % (i, fmt))
+        if fmt == "jpg":
+            from PIL import Image
+            Image.fromarray(img, "L").save(path, "JPEG", quality=quality)
+        elif fmt == "pgm":
+            with open(path, "wb") as f:
+                f.write(b"P5\n%d %d\n255\n" % (img.shape[1], img.shape[0]) + img.tobytes())
+        else:
+            raise ValueError(fmt)
+        _io.write_camera(os.path.join(folder, "cams", "%08d_cam.txt" % i), v.K, v.R, v.t, DEPTH_LINE[0],
+                         DEPTH_LINE[1], DEPTH_LINE[2], DEPTH_LINE[3])
+    sel = []
+    for i in range(len(scene.views)):
+        srcs = list(scene.pairs[i])[: num_src or len(scene.pairs[i])]
+        sel.append([(s, len(srcs) - k) for k, s in enumerate(srcs)])
+    _io.write_pair(os.path.join(folder, "pair.txt"), sel)

@@ -88,6 +88,34 @@ typedef struct acmmp_timing {
     float total_ms;         /* whole RunPatchMatch, device side */
 } acmmp_timing;
 
+/* == struct Problem (src/acmmp_definitions.h:57-63), fixed-size source list. */
+typedef struct acmmp_problem {
+    int32_t ref_image_id;
+    int32_t num_src_images;
+    int32_t src_image_ids[ACMMP_MAX_IMAGES - 1];
+    int32_t max_image_size;     /* 6400 until ComputeMultiScaleSettings */
+    int32_t num_downscale;
+    int32_t cur_image_size;     /* 6400 until the scale loop sets it */
+} acmmp_problem;
+
+/* The flags of ProcessProblem (src/acmmp_definitions.cpp:245-250) plus what the
+ * reference takes from globals: device (cudaSetDevice(0), :253), the RNG key
+ * (clock64() in the reference) and an iteration override. */
+typedef struct acmmp_pass_options {
+    int32_t device;
+    int32_t geom_consistency;
+    int32_t planar_prior;
+    int32_t hierarchy;
+    int32_t multi_geometry;
+    int32_t seeded;             /* pSampler priors (src/acmmp_definitions.cpp:8-177): not supported */
+    int32_t max_iterations;     /* <= 0: reference behaviour (2; SetGeomConsistencyParams forces 2) */
+    uint32_t seed_lo;           /* Philox key of this pass */
+    uint32_t seed_hi;
+    int32_t write_triangulation;/* write 2333_%08d/triangulation.png in planar passes (:310-330) */
+    int32_t verbose;            /* print the reference's progress lines to stdout */
+    int32_t reserved[5];
+} acmmp_pass_options;
+
 typedef struct acmmp_ctx acmmp_ctx;
 
 /* Fills the reference defaults of PatchMatchParams (src/ACMMP.h:32-56). */
@@ -260,6 +288,53 @@ int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checke
 int acmmp_device_count(void);
 /* Library build string (arch, flags). */
 const char *acmmp_version(void);
+
+/* ---- Pass driver: the reference's pipeline around RunPatchMatch
+ *      (src/acmmp_definitions.cpp:179-403, src/ACMMP.cpp:525-809), reading
+ *      <dense>/images/%08d.jpg, <dense>/cams/%08d_cam.txt, <dense>/pair.txt and
+ *      writing <out>/2333_%08d/{depths[_geom],normals,costs}.dmb. Host code in
+ *      the library; the compute runs through the engine above. ---- */
+
+/* ~ GenerateSampleList (src/acmmp_definitions.cpp:179-205): parse pair.txt,
+ * dropping sources with score <= 0. *count = number of problems. */
+int acmmp_generate_sample_list(const char *dense_folder, acmmp_problem *problems, int capacity, int *count);
+/* ~ ComputeMultiScaleSettings (src/acmmp_definitions.cpp:207-243): per problem
+ * max_image_size (capped at 3200) and num_downscale (halvings until <= 1000);
+ * *max_num_downscale = the largest. */
+int acmmp_compute_multiscale_settings(const char *dense_folder, acmmp_problem *problems, int count,
+                                      int *max_num_downscale);
+/* ~ ACMMP::InputInitialization (src/ACMMP.cpp:525-636): read the ref and source
+ * images and cameras of problems[idx], rescale each to its problem's
+ * cur_image_size (sources use problems[src_id], as the reference does), set
+ * the depth range, and in geometric passes load the depth maps of the
+ * previous pass. Parameters (geom / multi_geometry / hierarchy) must be set
+ * before. */
+int acmmp_input_initialization(acmmp_ctx *ctx, const char *dense_folder, const char *output_folder,
+                               const acmmp_problem *problems, int count, int idx);
+/* ~ ACMMP::CudaSpaceInitialization (src/ACMMP.cpp:638-809): previous-pass
+ * plane/cost state of the reference view (geometric passes) and the
+ * hierarchy inputs (low-res normals/costs + upsampled depth). */
+int acmmp_space_initialization(acmmp_ctx *ctx, const char *output_folder, const acmmp_problem *problem);
+/* ~ ProcessProblem (src/acmmp_definitions.cpp:245-403): one view of one pass,
+ * including the planar-prior second run, written as .dmb files. */
+int acmmp_process_problem(const char *dense_folder, const char *output_folder, const acmmp_problem *problems,
+                          int count, int idx, const acmmp_pass_options *options);
+/* ~ JointBilateralUpsampling (src/acmmp_definitions.cpp:405-438): upsample
+ * 2333_%08d/depths_geom.dmb to the image resized to acmmp_size, overwriting
+ * 2333_%08d/depths.dmb. */
+int acmmp_joint_bilateral_upsampling(const char *dense_folder, const char *output_folder,
+                                     const acmmp_problem *problem, int acmmp_size, int device);
+/* Message of the last failing driver call on this thread ("" when none). */
+const char *acmmp_pipeline_last_error(void);
+
+/* ~ ACMMP::GetReferenceImage (src/ACMMP.cpp:843-846): the (rescaled) reference
+ * image, width*height floats. */
+int acmmp_get_reference_image(acmmp_ctx *ctx, float *out, size_t n);
+/* ~ ACMMP::GetPriorPlaneParams (src/ACMMP.cpp:920-953) for one triangle
+ * (x1 y1 x2 y2 x3 y3) with the depths at its corners; host. */
+int acmmp_prior_plane_params(const acmmp_camera *cam, const int32_t *tri, const float *depths, float *out4);
+/* ~ ACMMP::GetDepthFromPlaneParam (src/ACMMP.cpp:955-958); host. */
+float acmmp_depth_from_plane_param(const acmmp_camera *cam, const float *plane4, int x, int y);
 
 /* ---- Reference on-disk formats (src/ACMMP.cpp:154-380,
  *      src/acmmp_definitions.cpp:179-205). Pure host code. ---- */
