@@ -56,3 +56,16 @@ def test_cli_matches_in_process_driver(dense):
             x = aio.read_dmb(os.path.join(aio.result_folder(a, v), name + ".dmb"))
             y = aio.read_dmb(os.path.join(aio.result_folder(b, v), name + ".dmb"))
             assert_bit_exact(y, x, f"CLI view {v} {name}")
+
+
+def test_multi_scale_jbu_hierarchy_matches_oracle(tmp_path):
+    """Two scales (1010x760 -> 505x380 first): photometric + planar and two
+    geometric passes at the coarse scale, then JBU, the hierarchy + planar
+    pass and two geometric passes at full size."""
+    d = str(tmp_path / "dense")
+    sc = scene.make_scene(num_views=3, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=1)
+    out = pipeline.run_sequential(d, "/ACMMP", write_triangulation=False)
+    maps = OraclePipeline(d).run_multi_scale("sequential")
+    assert _compare(out, maps) == 3 * 4
+    assert aio.read_dmb(os.path.join(aio.result_folder(out, 0), "depths_geom.dmb")).shape == (760, 1010)
