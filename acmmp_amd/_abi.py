@@ -190,6 +190,7 @@ SIGNATURES = {
     "acmmp_generate_sample_list": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
     "acmmp_compute_multiscale_settings": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
     "acmmp_input_initialization": (C.c_int, [_CTX, C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int]),
+    "acmmp_load_view": (C.c_int, [C.c_char_p, C.c_int, C.c_int, _FP, C.c_size_t, C.POINTER(Camera)]),
     "acmmp_space_initialization": (C.c_int, [_CTX, C.c_char_p, C.POINTER(Problem)]),
     "acmmp_process_problem": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int,
                                         C.POINTER(PassOptions)]),

@@ -174,9 +174,53 @@ int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
     return write_png_rgb(path, W, H, rgb);
 }
 
+// One view of InputInitialization (src/ACMMP.cpp:536-598): image + camera,
+// camera size from the image, rescaled to max_image_size when larger.
+int load_view(const std::string &dense, int id, int max_image_size, acmmp::Image &im, acmmp_camera &cam) {
+    int rc = load_image(image_path(dense, id), im);
+    if (rc) return rc;
+    const std::string cam_path = dense + "/cams/" + id8(id) + "_cam.txt";
+    rc = acmmp_read_camera(cam_path.c_str(), &cam);
+    if (rc) return fail(rc, "cannot read camera %s", cam_path.c_str());
+    cam.height = im.rows;
+    cam.width = im.cols;
+    if (im.cols <= max_image_size && im.rows <= max_image_size) return ACMMP_OK;
+    const float factor_x = static_cast<float>(max_image_size) / im.cols;
+    const float factor_y = static_cast<float>(max_image_size) / im.rows;
+    const float factor = std::min(factor_x, factor_y);
+    const int new_cols = (int)std::round(im.cols * factor);
+    const int new_rows = (int)std::round(im.rows * factor);
+    const float scale_x = new_cols / static_cast<float>(im.cols);
+    const float scale_y = new_rows / static_cast<float>(im.rows);
+    acmmp::Image scaled;
+    scaled.cols = new_cols;
+    scaled.rows = new_rows;
+    scaled.data.resize((size_t)new_cols * new_rows);
+    acmmp_resize_linear(im.data.data(), im.cols, im.rows, scaled.data.data(), new_cols, new_rows);
+    im = std::move(scaled);
+    cam.K[0] *= scale_x;
+    cam.K[2] *= scale_x;
+    cam.K[4] *= scale_y;
+    cam.K[5] *= scale_y;
+    cam.height = new_rows;
+    cam.width = new_cols;
+    return ACMMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int acmmp_load_view(const char *dense_folder, int image_id, int max_image_size, float *out, size_t capacity,
+                    acmmp_camera *cam) {
+    if (!dense_folder || !cam || max_image_size <= 0) return fail(ACMMP_ERR_ARG, "bad args");
+    acmmp::Image im;
+    const int rc = load_view(dense_folder, image_id, max_image_size, im, *cam);
+    if (rc) return rc;
+    if (!out || capacity < im.data.size()) return ACMMP_ERR_ARG;  // *cam carries the size
+    std::memcpy(out, im.data.data(), im.data.size() * sizeof(float));
+    return ACMMP_OK;
+}
 
 const char *acmmp_pipeline_last_error(void) { return g_err.c_str(); }
 
@@ -250,47 +294,15 @@ int acmmp_input_initialization(acmmp_ctx *ctx, const char *dense_folder, const c
     if (n < 2 || n > ACMMP_MAX_IMAGES) return fail(ACMMP_ERR_ARG, "view %d has %d sources", pr.ref_image_id, n - 1);
     std::vector<acmmp::Image> images((size_t)n);
     std::vector<acmmp_camera> cams((size_t)n);
+    // a source view uses the cur_image_size of the problem indexed by its
+    // image id, as the reference does (src/ACMMP.cpp:564-568)
     for (int i = 0; i < n; ++i) {
         const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
-        int rc = load_image(image_path(dense, id), images[(size_t)i]);
+        if (i > 0 && (id < 0 || id >= count))
+            return fail(ACMMP_ERR_ARG, "source id %d is not a problem index (pair.txt ids must be 0..n-1)", id);
+        const int max_image_size = i == 0 ? pr.cur_image_size : problems[id].cur_image_size;
+        const int rc = load_view(dense, id, max_image_size, images[(size_t)i], cams[(size_t)i]);
         if (rc) return rc;
-        const std::string cam_path = dense + "/cams/" + id8(id) + "_cam.txt";
-        rc = acmmp_read_camera(cam_path.c_str(), &cams[(size_t)i]);
-        if (rc) return fail(rc, "cannot read camera %s", cam_path.c_str());
-        cams[(size_t)i].height = images[(size_t)i].rows;
-        cams[(size_t)i].width = images[(size_t)i].cols;
-    }
-    // Scale cameras and images (src/ACMMP.cpp:564-598); a source view uses the
-    // cur_image_size of the problem indexed by its image id, as the reference does.
-    for (int i = 0; i < n; ++i) {
-        int max_image_size = pr.cur_image_size;
-        if (i > 0) {
-            const int sid = pr.src_image_ids[i - 1];
-            if (sid < 0 || sid >= count)
-                return fail(ACMMP_ERR_ARG, "source id %d is not a problem index (pair.txt ids must be 0..n-1)", sid);
-            max_image_size = problems[sid].cur_image_size;
-        }
-        acmmp::Image &im = images[(size_t)i];
-        if (im.cols <= max_image_size && im.rows <= max_image_size) continue;
-        const float factor_x = static_cast<float>(max_image_size) / im.cols;
-        const float factor_y = static_cast<float>(max_image_size) / im.rows;
-        const float factor = std::min(factor_x, factor_y);
-        const int new_cols = (int)std::round(im.cols * factor);
-        const int new_rows = (int)std::round(im.rows * factor);
-        const float scale_x = new_cols / static_cast<float>(im.cols);
-        const float scale_y = new_rows / static_cast<float>(im.rows);
-        acmmp::Image scaled;
-        scaled.cols = new_cols;
-        scaled.rows = new_rows;
-        scaled.data.resize((size_t)new_cols * new_rows);
-        acmmp_resize_linear(im.data.data(), im.cols, im.rows, scaled.data.data(), new_cols, new_rows);
-        im = std::move(scaled);
-        cams[(size_t)i].K[0] *= scale_x;
-        cams[(size_t)i].K[2] *= scale_x;
-        cams[(size_t)i].K[4] *= scale_y;
-        cams[(size_t)i].K[5] *= scale_y;
-        cams[(size_t)i].height = new_rows;
-        cams[(size_t)i].width = new_cols;
     }
     std::vector<const float *> ptrs((size_t)n);
     for (int i = 0; i < n; ++i) ptrs[(size_t)i] = images[(size_t)i].data.data();

@@ -1,0 +1,321 @@
+"""View-parallel pass driver: one process per GPU.
+
+Within a pass every view's RunPatchMatch is independent, so views are sharded
+across ranks (LPT on W*H*(N-1)) and each rank runs its views on its own GPU
+with no communication. Between passes the only data another view needs is
+source depth maps (src/ACMMP.cpp:608-635; used as depth_images[j+1] in
+src/ACMMP.cu:753, 1064, 1085), so each pass ends with ONE all-gather of the
+f32 depth maps (`all_gather_into_tensor` = RCCL over xGMI with the nccl
+backend; padded to the largest map since RCCL has no all-gatherv). Normals,
+costs and the planar/hierarchy inputs stay on the rank that owns the view.
+
+Schedule: Jacobi — every view of a pass reads the previous pass's maps. The
+reference's second geometric pass is Gauss-Seidel (src/main_ACMMP.cpp:
+159-172); the single-process drivers (`pipeline.run_sequential`, the
+acmmp_main CLI) keep that order, and tests/oracle_pipeline.py restates both.
+
+The pass / exchange logic is independent of the engine: `compute` and `jbu`
+are injectable, which is how the world-size-2 gloo tests exercise it on CPU.
+Outputs are the reference's .dmb files, written by the owning rank.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _abi
+from . import io as aio
+from . import pipeline
+from .engine import ACMMP, AcmmpError, joint_bilateral_upsample
+
+
+def lpt_assign(costs: list, world: int) -> list:
+    """Longest-processing-time-first: views sorted by cost (desc, then index)
+    go to the least-loaded rank (ties: lowest rank). Per-rank lists ascending."""
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for v in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(v)
+        load[r] += costs[v]
+    return [sorted(o) for o in out]
+
+
+class DepthExchange:
+    """All-gather of per-view depth maps of different sizes over a padded
+    [world * slots, Hmax, Wmax] buffer with all_gather_into_tensor."""
+
+    def __init__(self, assignment: list, shapes: dict, device: torch.device, group=None):
+        self.assignment = assignment
+        self.shapes = shapes
+        self.device = device
+        self.group = group
+        self.slots = max(1, max(len(a) for a in assignment))
+        self.hmax = max(h for h, _ in shapes.values())
+        self.wmax = max(w for _, w in shapes.values())
+
+    def gather(self, rank: int, local: dict) -> dict:
+        world = len(self.assignment)
+        send = torch.zeros((self.slots, self.hmax, self.wmax), dtype=torch.float32, device=self.device)
+        for k, v in enumerate(self.assignment[rank]):
+            h, w = self.shapes[v]
+            send[k, :h, :w] = local[v].to(self.device)
+        if world == 1:
+            recv = send
+        else:  # concatenated along dim 0: rank r's slots at [r * slots, (r + 1) * slots)
+            recv = torch.empty((world * self.slots, self.hmax, self.wmax), dtype=torch.float32, device=self.device)
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+        out = {}
+        for r in range(world):
+            for k, v in enumerate(self.assignment[r]):
+                h, w = self.shapes[v]
+                out[v] = recv[r * self.slots + k, :h, :w].contiguous()
+        return out
+
+
+@dataclass
+class ViewTask:
+    """Everything one ProcessProblem call needs, in memory."""
+    index: int                 # problem index
+    ref_id: int
+    ids: list                  # image ids, ref first
+    cams: list                 # acmmp_camera per image (rescaled)
+    images: list               # float32 tensors (H, W) per image
+    geom: bool
+    planar: bool
+    hierarchy: bool
+    multi: bool
+    seed_lo: int
+    seed_hi: int
+    max_iterations: int
+    depths: Optional[list] = None          # source depth maps (tensors) for geom passes
+    state: Optional[tuple] = None          # (planes (H,W,4), costs (H,W)) numpy, geom passes
+    hier_inputs: Optional[tuple] = None    # (scaled planes (sh,sw,4), upsampled depth (H,W)) numpy
+
+
+@dataclass
+class ViewResult:
+    planes: np.ndarray   # (H, W, 4): world normal xyz + depth
+    costs: np.ndarray    # (H, W)
+    extra: dict = field(default_factory=dict)
+
+
+def engine_compute(device: int) -> Callable[[ViewTask], ViewResult]:
+    """ProcessProblem's per-view work (src/acmmp_definitions.cpp:260-379) on
+    the GPU engine, with images / depth maps borrowed from HBM."""
+
+    def run(t: ViewTask) -> ViewResult:
+        with ACMMP(device) as eng:
+            if t.geom:
+                eng.SetGeomConsistencyParams(t.multi)
+            if t.hierarchy:
+                eng.SetHierarchyParams()
+            eng.update_params(seed_lo=t.seed_lo & 0xFFFFFFFF, seed_hi=t.seed_hi & 0xFFFFFFFF)
+            if t.max_iterations > 0:
+                eng.update_params(max_iterations=t.max_iterations)
+            eng.set_images_device(t.cams, [im.data_ptr() for im in t.images])
+            if t.geom:
+                eng.set_depth_maps_device([d.data_ptr() for d in t.depths])
+                eng.set_plane_hypotheses(*t.state)
+            if t.hierarchy:
+                eng.set_hierarchy_inputs(*t.hier_inputs)
+            eng.RunPatchMatch()
+            if t.planar:
+                eng.prepare_planar_prior()
+                eng.RunPatchMatch()
+            return ViewResult(eng.plane_hypotheses(), eng.costs())
+
+    return run
+
+
+def gpu_jbu(device: int):
+    def run(image: np.ndarray, depth: np.ndarray):
+        return joint_bilateral_upsample(image, depth, device)
+    return run
+
+
+class ViewParallelPipeline:
+    """main_ACMMP's multi-scale pass loop (src/main_ACMMP.cpp:96-176), views
+    sharded over the ranks of `group` (default: the world)."""
+
+    def __init__(self, dense_folder: str, output_dir: str = "/ACMMP", device: int = 0, seed: int = 1234,
+                 max_iterations: int = 0, geom_iterations: int = 2, group=None,
+                 compute: Optional[Callable] = None, jbu: Optional[Callable] = None, write_outputs: bool = True,
+                 comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None):
+        self.dense = dense_folder
+        self.output_folder = dense_folder + output_dir
+        self.device = device
+        self.seed = seed
+        self.max_iterations = max_iterations
+        self.geom_iterations = geom_iterations
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.compute = compute or engine_compute(device)
+        self.jbu = jbu or gpu_jbu(device)
+        self.write_outputs = write_outputs
+        if tensor_device is None:
+            tensor_device = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
+        self.tdev = tensor_device
+        if comm_device is None:
+            backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+            comm_device = self.tdev if backend == "nccl" else torch.device("cpu")
+        self.cdev = comm_device
+        self.problems = pipeline.generate_sample_list(dense_folder)
+        self.index_of = {p.ref_image_id: i for i, p in enumerate(self.problems)}
+        self.max_num_downscale = pipeline.compute_multiscale_settings(dense_folder, self.problems)
+        costs = []
+        for p in self.problems:
+            w, h = aio.image_size(self._image_path(p.ref_image_id))
+            costs.append(float(w * h * max(p.num_src_images, 1)))
+        self.assignment = lpt_assign(costs, self.world)
+        self.mine = self.assignment[self.rank]
+        self.state = {}     # own views: ref_id -> ViewResult (latest pass)
+        self.depths = {}    # every view: ref_id -> depth tensor (previous pass, gathered)
+        self.pass_index = 0
+
+    # ------------------------------------------------------------- inputs
+    def _image_path(self, image_id: int) -> str:
+        base = os.path.join(self.dense, "images", "%08d" % image_id)
+        for ext in (".jpg", ".pgm", ".pfm"):
+            if os.path.exists(base + ext):
+                return base + ext
+        return base + ".jpg"
+
+    def _load_views(self):
+        """Images + cameras of every image my views need, at their problem's
+        cur_image_size (InputInitialization, src/ACMMP.cpp:536-598)."""
+        import ctypes as C
+        lib = _abi.load_library()
+        need = set()
+        for v in self.mine:
+            p = self.problems[v]
+            need.add(p.ref_image_id)
+            need.update(p.sources)
+        self.images, self.cams = {}, {}
+        for i in sorted(need):
+            if i not in self.index_of:
+                raise AcmmpError(f"source id {i} is not a problem index (pair.txt ids must be 0..n-1)")
+            size = self.problems[self.index_of[i]].cur_image_size
+            cam = _abi.Camera()
+            rc = lib.acmmp_load_view(self.dense.encode(), i, size, None, 0, C.byref(cam))
+            if rc not in (0, _abi.ERR_ARG):
+                raise AcmmpError(f"acmmp_load_view({i}) failed: {lib.acmmp_pipeline_last_error().decode()}")
+            img = np.empty((cam.height, cam.width), dtype=np.float32)
+            rc = lib.acmmp_load_view(self.dense.encode(), i, size, img.ctypes.data_as(C.POINTER(C.c_float)),
+                                     img.size, C.byref(cam))
+            if rc != 0:
+                raise AcmmpError(f"acmmp_load_view({i}) failed: {lib.acmmp_pipeline_last_error().decode()}")
+            self.images[i] = torch.from_numpy(img).to(self.tdev)
+            self.cams[i] = cam
+
+    def _shapes(self):
+        shapes = {}
+        for i, p in enumerate(self.problems):
+            w, h = aio.image_size(self._image_path(p.ref_image_id))
+            m = p.cur_image_size
+            if w > m or h > m:
+                f = min(np.float32(m) / np.float32(w), np.float32(m) / np.float32(h))
+                w, h = int(np.round(np.float32(w) * f)), int(np.round(np.float32(h) * f))
+            shapes[i] = (h, w)
+        return shapes
+
+    # --------------------------------------------------------------- pass
+    def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
+        local = {}
+        for v in self.mine:
+            p = self.problems[v]
+            ids = [p.ref_image_id] + p.sources
+            t = ViewTask(index=v, ref_id=p.ref_image_id, ids=ids, cams=[self.cams[i] for i in ids],
+                         images=[self.images[i] for i in ids], geom=geom, planar=planar, hierarchy=hierarchy,
+                         multi=multi, seed_lo=self.seed + p.ref_image_id, seed_hi=self.pass_index,
+                         max_iterations=self.max_iterations)
+            if geom:
+                t.depths = [self.depths[self.index_of[i]].to(self.tdev) for i in ids]
+                prev = self.state[v]
+                t.state = (prev.planes, prev.costs)
+            if hierarchy:
+                prev = self.state[v]
+                H, W = t.images[0].shape
+                up = prev.extra["jbu_depth"]
+                sh, sw = prev.costs.shape
+                upsample = sw != H or sh != W  # src/ACMMP.cpp:766, rows/cols swap included
+                w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
+                scaled = np.concatenate([prev.planes[..., :3], w[..., None]], -1).astype(np.float32)
+                t.hier_inputs = (scaled, up)
+            res = self.compute(t)
+            self.state[v] = res
+            local[v] = torch.from_numpy(np.ascontiguousarray(res.planes[..., 3]))
+            if self.write_outputs:
+                self._write(p.ref_image_id, res, geom)
+        self.depths = exchange.gather(self.rank, local)
+        self.pass_index += 1
+
+    def _write(self, ref_id: int, res: ViewResult, geom: bool):
+        folder = aio.result_folder(self.output_folder, ref_id)
+        os.makedirs(folder, exist_ok=True)
+        aio.write_dmb(os.path.join(folder, "depths_geom.dmb" if geom else "depths.dmb"), res.planes[..., 3])
+        aio.write_dmb(os.path.join(folder, "normals.dmb"), res.planes[..., :3])
+        aio.write_dmb(os.path.join(folder, "costs.dmb"), res.costs)
+
+    def run(self) -> str:
+        os.makedirs(self.output_folder, exist_ok=True)
+        max_down = self.max_num_downscale
+        first = True
+        while max_down >= 0:
+            pipeline.scale_step(self.problems)
+            self._load_views()
+            exchange = DepthExchange(self.assignment, self._shapes(), self.cdev, self.group)
+            if first:
+                first = False
+                self.run_pass(False, True, False, False, exchange)
+            else:
+                for v in self.mine:  # JointBilateralUpsampling, in memory
+                    p = self.problems[v]
+                    img = self.images[p.ref_image_id].cpu().numpy()
+                    up, isc = self.jbu(img, self.state[v].planes[..., 3])
+                    if up is None:
+                        raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
+                    self.state[v].extra["jbu_depth"] = up
+                self.run_pass(False, True, True, False, exchange)
+            for g in range(self.geom_iterations):
+                self.run_pass(True, False, False, g > 0, exchange)
+            max_down -= 1
+        if dist.is_initialized() and self.world > 1:
+            dist.barrier(group=self.group)
+        return self.output_folder
+
+
+def main():
+    """python -m torch.distributed.run --nproc-per-node N -m acmmp_amd.distributed <dense_folder> [...]"""
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("dense_folder")
+    ap.add_argument("--output_dir", default="/ACMMP")
+    ap.add_argument("--iterations", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--backend", default=None, help="nccl (RCCL, default with GPUs) or gloo")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        backend = args.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend)
+    pipe = ViewParallelPipeline(args.dense_folder, args.output_dir, device=local_rank, seed=args.seed,
+                                max_iterations=args.iterations)
+    out = pipe.run()
+    if pipe.rank == 0:
+        print(f"Depth/normal/cost maps written under {out}")
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

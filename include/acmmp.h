@@ -311,6 +311,13 @@ int acmmp_compute_multiscale_settings(const char *dense_folder, acmmp_problem *p
  * before. */
 int acmmp_input_initialization(acmmp_ctx *ctx, const char *dense_folder, const char *output_folder,
                                const acmmp_problem *problems, int count, int idx);
+/* One view of InputInitialization (src/ACMMP.cpp:536-598): reads
+ * images/%08d.jpg and cams/%08d_cam.txt of `image_id`, sets the camera's size
+ * and rescales image + K to max_image_size when larger. *cam is always
+ * filled on success of the read; `out` receives cam->width*cam->height floats
+ * when capacity suffices (else ACMMP_ERR_ARG). */
+int acmmp_load_view(const char *dense_folder, int image_id, int max_image_size, float *out, size_t capacity,
+                    acmmp_camera *cam);
 /* ~ ACMMP::CudaSpaceInitialization (src/ACMMP.cpp:638-809): previous-pass
  * plane/cost state of the reference view (geometric passes) and the
  * hierarchy inputs (low-res normals/costs + upsampled depth). */
