@@ -37,6 +37,19 @@ struct Image {  // cv::Mat_<float>, row-major
 using Problem = acmmp_problem;  // struct Problem (src/acmmp_definitions.h:57-63)
 using Camera = acmmp_camera;    // struct Camera (src/acmmp_definitions.h:47-55)
 
+// struct Problem with a std::vector of sources -> the fixed-size C layout
+inline Problem make_problem(int ref_image_id, const std::vector<int> &src_image_ids, int max_image_size = 6400,
+                            int num_downscale = 0, int cur_image_size = 6400) {
+    Problem p{};
+    p.ref_image_id = ref_image_id;
+    for (int id : src_image_ids)
+        if (p.num_src_images < ACMMP_MAX_IMAGES - 1) p.src_image_ids[p.num_src_images++] = id;
+    p.max_image_size = max_image_size;
+    p.num_downscale = num_downscale;
+    p.cur_image_size = cur_image_size;
+    return p;
+}
+
 class Error : public std::runtime_error {
    public:
     Error(const std::string &what, int status) : std::runtime_error(what), status_(status) {}

@@ -127,3 +127,40 @@ def test_camera_writer_roundtrip(tmp_path, lib):
     assert lib.acmmp_read_camera(path.encode(), C.byref(cam)) == 0
     assert (cam.depth_min, cam.depth_max) == (300.0, 800.0)
     np.testing.assert_allclose(np.array(cam.t), t, rtol=1e-7)
+
+
+def test_cpp_class_shim_compiles_and_links(tmp_path):
+    """include/acmmp.hpp (the C++ `class ACMMP` surface) builds against the
+    library; host-only calls work without a GPU, engine creation fails loudly."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "shim.cpp"
+    src.write_text(r'''
+#include <acmmp.hpp>
+#include <cstdio>
+int main() {
+    acmmp::Problem p = acmmp::make_problem(3, {1, 2, 4});
+    int32_t xy[10] = {0, 0, 10, 0, 0, 10, 10, 10, 5, 4};
+    int32_t t[6 * 32];
+    int n = 0;
+    int rc = acmmp_delaunay_triangulation(20, 20, xy, 5, t, 32, &n);
+    bool threw = false;
+    if (acmmp_device_count() == 0) {
+        try { acmmp::ACMMP a(0); } catch (const acmmp::Error &e) { threw = true; }
+    } else {
+        threw = true;
+    }
+    std::printf("%d %d %d %d\n", p.num_src_images, rc, n, threw ? 1 : 0);
+    return 0;
+}
+''')
+    exe = tmp_path / "shim"
+    lib = os.path.join(root, "acmmp_amd", "lib")
+    subprocess.run([gxx, "-std=c++17", "-I" + os.path.join(root, "include"), str(src), "-L" + lib, "-lacmmp_amd",
+                    "-Wl,-rpath," + lib, "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["3", "0", "4", "1"]
