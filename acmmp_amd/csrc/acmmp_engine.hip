@@ -254,8 +254,8 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
     }
     for (int i = 0; i < num_images; ++i) {
         const int w = cams[i].width, h = cams[i].height;
-        const int pp = (w + 3 + 31) / 32 * 32;
-        const size_t bytes = (size_t)pp * (h + 3) * sizeof(float);
+        const int pp = (w + 3 + 15) / 16 * 16;  // float pairs per row (128-B rows)
+        const size_t bytes = (size_t)pp * (h + 2) * 2 * sizeof(float);
         if (ctx->pad_bytes[i] < bytes) {
             HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
             ctx->pad_bytes[i] = bytes;
@@ -760,6 +760,17 @@ int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checke
     (void)hipFree(d);
     return rc;
 }
+
+#ifdef ACMMP_DIAG_PROBE
+// Diagnostic builds only: split-kernel NCC throughput probe on the current state.
+int acmmp_diag_probe(acmmp_ctx *ctx, int variant, int reps, float *ms) {
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    rc = kv_upload(ctx);
+    if (rc) return rc;
+    return probe_run(ctx->d_kv, ctx->h_kv, state_of(ctx), variant, reps, ms, ctx->stream);
+}
+#endif
 
 // Diagnostic builds only (ACMMP_DIAG_STAMPS); not declared in include/acmmp.h.
 int acmmp_diag_read_cycles(uint64_t *out8) {

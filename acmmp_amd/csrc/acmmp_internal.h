@@ -36,12 +36,13 @@ struct KViews {
     ViewRel rel[ACMMP_MAX_IMAGES];            // rel[v] for source v (1-based), rel[0] unused
     const float *img[ACMMP_MAX_IMAGES];       // pitched images
     int ipitch[ACMMP_MAX_IMAGES];             // in floats
-    // Source images with clamp-to-edge baked in: element (r, c) holds texel
-    // (clamp(c - 1), clamp(r - 1)), (W + 3) x (H + 3), so every bilinear
-    // footprint of a coordinate clamped to [-1, W] x [-1, H] is addressable
-    // without integer clamps or selects.
+    // Source images with clamp-to-edge baked in, row-paired: element (r, c)
+    // (r < H + 2, c < W + 3) is the float pair (texel(clamp(c-1), clamp(r-1)),
+    // texel(clamp(c-1), clamp(r))), so the 2x2 bilinear footprint of a
+    // coordinate clamped to [-1, W] x [-1, H] is ONE 16-byte load, without
+    // integer clamps or selects.
     const float *pad[ACMMP_MAX_IMAGES];
-    int ppitch[ACMMP_MAX_IMAGES];
+    int ppitch[ACMMP_MAX_IMAGES];             // in float pairs
     const float *dep[ACMMP_MAX_IMAGES];       // pitched depth maps (geom consistency)
     int dpitch[ACMMP_MAX_IMAGES];
     int dw[ACMMP_MAX_IMAGES];
@@ -84,6 +85,8 @@ hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4
 hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch,
                             hipStream_t stream);
 int diag_read_cycles(unsigned long long *out8);
+int probe_run(const KViews *d_kv, const KViews &h_kv, const KState &st, int variant, int reps, float *ms,
+              hipStream_t s);
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);

@@ -283,7 +283,7 @@ DEV SrcImage src_image(const KViews &kv, int v) {
     s.pitch = kv.ppitch[v];
     s.W = kv.cam[v].width;
     s.H = kv.cam[v].height;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)0, s.pitch * (s.H + 3) * 4, 0x00020000);
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)0, s.pitch * (s.H + 2) * 8, 0x00020000);
     return s;
 }
 
@@ -367,41 +367,61 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
 
 // Fetch stage of one patch column (fixed x = px - 5 + 2 ii) of the source
 // samples: projection (pin P1, the x-term hoisted per column), the coordinate
-// clamp of pin P2, and two 8-byte texel-pair loads per sample from the padded
-// image (rows y0 and y0 + 1; padded element (y0 + 1, x0 + 1) is texel
-// (clamp(x0), clamp(y0))).
+// clamp of pin P2, and ONE 16-byte load per sample of the 2x2 bilinear
+// footprint from the row-paired padded image (element (r, c) holds the
+// texels of rows r-1 and r at column c-1, clamp-to-edge, so the load at
+// (y0 + 1, x0 + 1) returns (t00, t01, t10, t11) = texels (x0,y0), (x0,y0+1),
+// (x0+1,y0), (x0+1,y0+1)). The x/y halves of the projection and of the
+// coordinate arithmetic run as packed-FP32 pairs (v_pk_fma / v_pk_mul /
+// v_pk_add: the same IEEE operation per component as the scalar pin).
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 struct ColFetch {
-    u32x2 t0[kTaps], t1[kTaps];  // texel pairs of rows y0, y0 + 1
+    u32x4 t[kTaps];               // (t00, t01, t10, t11) per sample
     float ax[kTaps], ay[kTaps];   // bilinear weights
 };
 
+DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <bool FAST>
 DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFetch &f) {
-    const float cx = dm_fma(H[0], x, H[2]);
-    const float cy = dm_fma(H[3], x, H[5]);
+    const f2v cxy = fma2(f2v{H[0], H[3]}, f2v{x, x}, f2v{H[2], H[5]});
     const float cz = dm_fma(H[6], x, H[8]);
+    const f2v h14 = f2v{H[1], H[4]};
     const float fw = (float)im.W, fh = (float)im.H;
-    const int row_bytes = im.pitch * 4;
 #pragma unroll
     for (int jj = 0; jj < kTaps; ++jj) {
         const float y = (float)(py - 5 + 2 * jj);
-        const float hx = dm_fma(H[1], y, cx);
-        const float hy = dm_fma(H[4], y, cy);
+        const f2v hxy = fma2(h14, f2v{y, y}, cxy);
         const float hz = dm_fma(H[7], y, cz);
         const float inv = recip<FAST>(hz);
-        float xs = (hx * inv + 0.5f) - 0.5f;
-        float ys = (hy * inv + 0.5f) - 0.5f;
-        // clamp to [-1, W] x [-1, H]: v_max/v_min (NaN -> -1; bounds are
-        // never +-0, so no signed-zero ambiguity) == the oracle's selects
-        xs = fminf(fmaxf(xs, -1.0f), fw);
-        ys = fminf(fmaxf(ys, -1.0f), fh);
-        const float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
-        f.ax[jj] = xs - fx0;
-        f.ay[jj] = ys - fy0;
-        const int off = (int)(__umul24((unsigned)((int)fy0 + 1), (unsigned)im.pitch) + (unsigned)((int)fx0 + 1)) * 4;
-        f.t0[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, off, 0, 0);
-        f.t1[jj] = __builtin_amdgcn_raw_buffer_load_b64(im.rsrc, off, row_bytes, 0);
+        f2v uv = hxy * f2v{inv, inv};
+        uv = (uv + 0.5f) - 0.5f;
+        // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
+        // (finite homography, |hz| inside the reciprocal window), where
+        // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
+        // bounds are never +-0) == the oracle's selects.
+        const float xs = FAST ? __builtin_amdgcn_fmed3f(uv.x, -1.0f, fw) : fminf(fmaxf(uv.x, -1.0f), fw);
+        const float ys = FAST ? __builtin_amdgcn_fmed3f(uv.y, -1.0f, fh) : fminf(fmaxf(uv.y, -1.0f), fh);
+        const f2v fl = f2v{dm_floor(xs), dm_floor(ys)};
+        const f2v a = f2v{xs, ys} - fl;
+        f.ax[jj] = a.x;
+        f.ay[jj] = a.y;
+        const int off = (int)(__umul24((unsigned)((int)fl.y + 1), (unsigned)im.pitch) + (unsigned)((int)fl.x + 1)) * 8;
+        f.t[jj] = __builtin_amdgcn_raw_buffer_load_b128(im.rsrc, off, 0, 0);
     }
+}
+
+// Bilinear value of a fetched sample (pin P2's lerp order):
+// top = fma(ax, t10 - t00, t00), bot = fma(ax, t11 - t01, t01) as one packed
+// pair, then fma(ay, bot - top, top).
+DEV float bilinear_sample(const ColFetch &f, int jj) {
+    const u32x4 t = f.t[jj];
+    const f2v lo = f2v{__uint_as_float(t.x), __uint_as_float(t.y)};
+    const f2v hi = f2v{__uint_as_float(t.z), __uint_as_float(t.w)};
+    const f2v tb = fma2(f2v{f.ax[jj], f.ax[jj]}, hi - lo, lo);
+    return dm_fma(f.ay[jj], tb.y - tb.x, tb.x);
 }
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
@@ -433,24 +453,21 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
         ColFetch f;
         fetch_column<FAST>(im, H, (float)(px - 5 + 2 * ii), py, f);
 #endif
-        float r_s = 0.0f, r_ss = 0.0f, r_rs = 0.0f;
+        // per column: r_s += ws; (r_ss, r_rs) = fma((ws, wr), sv, (r_ss, r_rs))
+        float r_s = 0.0f;
+        f2v racc = f2v{0.0f, 0.0f};
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const float t00 = __uint_as_float(f.t0[jj].x), t10 = __uint_as_float(f.t0[jj].y);
-            const float t01 = __uint_as_float(f.t1[jj].x), t11 = __uint_as_float(f.t1[jj].y);
-            const float top = dm_fma(f.ax[jj], t10 - t00, t00);
-            const float bot = dm_fma(f.ax[jj], t11 - t01, t01);
-            const float sv = dm_fma(f.ay[jj], bot - top, top);
+            const float sv = bilinear_sample(f, jj);
             const float w = wl[(ii * kTaps + jj) * kThreads];
             const float wr = w * tile[tb + ii + 2 * kTileW * jj];
             const float ws = w * sv;
             r_s += ws;
-            r_ss = dm_fma(ws, sv, r_ss);
-            r_rs = dm_fma(wr, sv, r_rs);
+            racc = fma2(f2v{ws, wr}, f2v{sv, sv}, racc);
         }
         sum_src += r_s;
-        sum_ss += r_ss;
-        sum_rs += r_rs;
+        sum_ss += racc.x;
+        sum_rs += racc.y;
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -1343,17 +1360,21 @@ __global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kv
 }
 
 // Padded copy of a source image (see KViews::pad).
+// Row-paired clamp-to-edge copy of a source view for the NCC gathers:
+// element (r, c), r < H + 2, c < W + 3, is the float pair
+// (texel(clamp(c-1), clamp(r-1)), texel(clamp(c-1), clamp(r))); dpitch in pairs.
 __global__ __launch_bounds__(256) void k_pad_image(const float *__restrict__ src, int spitch, int W, int H,
                                                    float *__restrict__ dst, int dpitch) {
     const int c = blockIdx.x * 64 + threadIdx.x;
     const int r = blockIdx.y * 4 + threadIdx.y;
-    if (c >= W + 3 || r >= H + 3) return;
-    const int x = min(max(c - 1, 0), W - 1), y = min(max(r - 1, 0), H - 1);
-    dst[r * dpitch + c] = src[y * spitch + x];
+    if (c >= W + 3 || r >= H + 2) return;
+    const int x = min(max(c - 1, 0), W - 1);
+    const int y0 = min(max(r - 1, 0), H - 1), y1 = min(r, H - 1);
+    reinterpret_cast<float2 *>(dst)[(size_t)r * dpitch + c] = make_float2(src[y0 * spitch + x], src[y1 * spitch + x]);
 }
 
 hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch, hipStream_t s) {
-    dim3 block(64, 4), grid((W + 3 + 63) / 64, (H + 3 + 3) / 4);
+    dim3 block(64, 4), grid((W + 3 + 63) / 64, (H + 2 + 3) / 4);
     k_pad_image<<<grid, block, 0, s>>>(src, spitch, W, H, dst, dpitch);
     return hipGetLastError();
 }
@@ -1431,6 +1452,146 @@ __global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int 
     }
     out[(size_t)py * W + px] = total_val / normalizing_factor;
 }
+
+#ifdef ACMMP_DIAG_PROBE
+// ---- throughput probe (diagnostic builds only): one thread per (pixel,
+// candidate), the pixel's 36 (w, w*r) pairs precomputed and staged in LDS,
+// NCC against every source view; measures the split-kernel design.
+__global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ kvp, int colour, float2 *wpair,
+                                                    float4 *stats, int P2) {
+    __shared__ float tile[kTileW * kTileH];
+    __shared__ float wlds[kSamples * kThreads];
+    const KViews &kv = *kvp;
+    const BlockXY blk{(int)blockIdx.x, (int)blockIdx.y};
+    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    __syncthreads();
+    const LaneGeom g = lane_geom(colour, blk);
+    if (g.py >= kv.H || g.px >= kv.W) return;
+    PixPatch pp;
+    pp.wo = threadIdx.y * kBX + threadIdx.x;
+    pp.w = wlds + pp.wo;
+    pixel_patch(kv, tile, g.tb, g.s, pp);
+    const int my = g.py * kv.Wh + g.k;
+    for (int ii = 0; ii < kTaps; ++ii)
+        for (int jj = 0; jj < kTaps; ++jj) {
+            const float w = pp.w[(ii * kTaps + jj) * kThreads];
+            wpair[(size_t)(ii * kTaps + jj) * P2 + my] = make_float2(w, w * tile[g.tb + ii + 2 * kTileW * jj]);
+        }
+    stats[my] = make_float4(pp.mean, pp.var, pp.inv_wsum, 0.0f);
+}
+
+template <bool FAST, int PIPE>
+DEV void ncc_sums_lean(const SrcImage &im, const float *H, const float2 (*wl)[64], int lane, int px, int py,
+                       float &sum_src, float &sum_ss, float &sum_rs) {
+    sum_src = sum_ss = sum_rs = 0.0f;
+    ColFetch buf[PIPE ? 2 : 1];
+    if (PIPE) fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        if (PIPE) {
+            if (ii + 1 < kTaps) fetch_column<FAST>(im, H, (float)(px - 5 + 2 * (ii + 1)), py, buf[(ii + 1) & 1]);
+        } else {
+            fetch_column<FAST>(im, H, (float)(px - 5 + 2 * ii), py, buf[0]);
+        }
+        const ColFetch &f = buf[PIPE ? (ii & 1) : 0];
+        float r_s = 0.0f;
+        f2v racc = f2v{0.0f, 0.0f};
+#pragma unroll
+        for (int jj = 0; jj < kTaps; ++jj) {
+            const float sv = bilinear_sample(f, jj);
+            const float2 w = wl[ii * kTaps + jj][lane];
+            const float ws = w.x * sv;
+            r_s += ws;
+            racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
+        }
+        sum_src += r_s;
+        sum_ss += racc.x;
+        sum_rs += racc.y;
+    }
+}
+
+template <int PIPE>
+__global__ __launch_bounds__(576) void k_probe(const KViews *__restrict__ kvp, KState st, int colour,
+                                                const float2 *__restrict__ wpair, const float4 *__restrict__ stats,
+                                                int P2, float *__restrict__ out) {
+    __shared__ float2 wl[kSamples][64];
+    const KViews &kv = *kvp;
+    const int lane = threadIdx.x, d = threadIdx.y;
+    const int k = blockIdx.x * 64 + lane, py = blockIdx.y;
+    const int Wh = kv.Wh;
+    for (int e = d * 64 + lane; e < kSamples * 64; e += 576) {
+        const int kk = blockIdx.x * 64 + (e & 63);
+        wl[e >> 6][e & 63] = kk < Wh ? wpair[(size_t)(e >> 6) * P2 + py * Wh + kk] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    const int s = (py + colour) & 1;
+    const int px = 2 * k + s;
+    if (px >= kv.W) return;
+    const int my = py * Wh + k;
+    const float4 ps = stats[my];
+    const int dx[9] = {0, 0, -3, 3, -1, 1, 0, 0, 0};
+    const int dy[9] = {-3, 3, 0, 0, 0, 0, -1, 1, 0};
+    const int nx = min(max(px + dx[d], 0), kv.W - 1), ny = min(max(py + dy[d], 0), kv.H - 1);
+    const float4 h = d == 8 ? st.plane[colour][my] : st.plane[colour ^ 1][ny * Wh + (nx >> 1)];
+    for (int v = 1; v <= kv.nsrc; ++v) {
+        float c = 2.0f;
+        if (ps.y >= 1e-5f) {
+            const SrcImage im = src_image(kv, v);
+            float H[9];
+            homography(kv, v, h, H);
+            const float2 pt = project(H, (float)px, (float)py);
+            if (!(pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f)) {
+                float sum_src, sum_ss, sum_rs;
+                ncc_sums_lean<true, PIPE>(im, H, wl, lane, px, py, sum_src, sum_ss, sum_rs);
+                sum_src *= ps.z;
+                sum_ss *= ps.z;
+                sum_rs *= ps.z;
+                const float var_src = sum_ss - sum_src * sum_src;
+                if (var_src >= 1e-5f) {
+                    const float covar = sum_rs - ps.x * sum_src;
+                    c = 1.0f - covar / dm_sqrt(ps.y * var_src);
+                    c = fminf(fmaxf(c, 0.0f), 2.0f);
+                }
+            }
+        }
+        out[(size_t)(d * 9 + v - 1) * P2 + my] = c;
+    }
+}
+
+static dim3 cs_grid(const KViews &kv, int colours);
+int probe_run(const KViews *d_kv, const KViews &h_kv, const KState &st, int variant, int reps, float *ms,
+              hipStream_t s) {
+    const int P2 = h_kv.H * h_kv.Wh;
+    float2 *wpair = nullptr;
+    float4 *stats = nullptr;
+    float *out = nullptr;
+    if (hipMalloc(&wpair, (size_t)kSamples * P2 * sizeof(float2)) != hipSuccess) return -3;
+    if (hipMalloc(&stats, (size_t)P2 * sizeof(float4)) != hipSuccess) return -3;
+    if (hipMalloc(&out, (size_t)81 * P2 * sizeof(float)) != hipSuccess) return -3;
+    k_probe_prep<<<cs_grid(h_kv, 1), dim3(kBX, kBY), 0, s>>>(d_kv, 0, wpair, stats, P2);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    dim3 grid((h_kv.Wh + 63) / 64, h_kv.H), block(64, 9);
+    for (int w = 0; w < 2; ++w) {
+        if (variant == 0) k_probe<0><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+        else k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+    }
+    hipEventRecord(a, s);
+    for (int r = 0; r < reps; ++r) {
+        if (variant == 0) k_probe<0><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+        else k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+    }
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(ms, a, b);
+    *ms /= reps;
+    hipFree(wpair);
+    hipFree(stats);
+    hipFree(out);
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
