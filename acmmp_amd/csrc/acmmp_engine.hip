@@ -256,6 +256,10 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         const int w = cams[i].width, h = cams[i].height;
         const int pp = (w + 3 + 15) / 16 * 16;  // float pairs per row (128-B rows)
         const size_t bytes = (size_t)pp * (h + 2) * 2 * sizeof(float);
+        // the gather kernels form record indices in fp32 (exact below 2^24):
+        // up to ~4090 x 4090 per view, above the reference's 3200 cap
+        if ((size_t)pp * (h + 2) >= (1u << 24))
+            return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^24-record gather limit", i, w, h);
         if (ctx->pad_bytes[i] < bytes) {
             HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
             ctx->pad_bytes[i] = bytes;

@@ -276,6 +276,7 @@ DEV float2 project(const float *H, float x, float y) {
 struct SrcImage {
     __amdgpu_buffer_rsrc_t rsrc;
     int pitch, W, H;
+    float fpitch, fp1;  // pitch and pitch + 1 as floats (exact: < 2^24)
 };
 
 DEV SrcImage src_image(const KViews &kv, int v) {
@@ -283,7 +284,10 @@ DEV SrcImage src_image(const KViews &kv, int v) {
     s.pitch = kv.ppitch[v];
     s.W = kv.cam[v].width;
     s.H = kv.cam[v].height;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)0, s.pitch * (s.H + 2) * 8, 0x00020000);
+    // structured view: 8-byte records (one row pair), indexed loads (idxen)
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)8, s.pitch * (s.H + 2), 0x00020000);
+    s.fp1 = (float)(s.pitch + 1);
+    s.fpitch = (float)s.pitch;
     return s;
 }
 
@@ -316,17 +320,18 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // normalised ref mean / variance — identical for all 14*(N-1) calls of a
 // pixel-iteration, so computed once (same operations, same order).
 struct PixPatch {
-    float *w;        // LDS: w[k * kThreads] for sample k of this lane (kThreads-strided)
+    float2 *w;       // LDS: (w, w * ref) at [k * kThreads] for sample k of this lane
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
     float inv_wsum;  // inv_bilateral_weight_sum
 };
 
-// The 36 weights live in LDS, one 256-float row per sample index k, so a
-// wave's read of weight k is 64 consecutive dwords (conflict-free) and the
-// weights cost no VGPRs: 36 KB + the 3.9 KB tile per 256-thread block lets 4
-// blocks (16 waves) share a CU.
+// The 36 weights live in LDS with their products w * ref (the reference
+// half of every NCC term is view-invariant), one 256-pair row per sample
+// index k, so a wave's read of sample k is one conflict-free ds_read_b64 and
+// costs no VGPRs: 72 KB + the 3.9 KB tile per 256-thread block (2 blocks =
+// the 8 waves of a CU at this kernel's occupancy).
 constexpr int kThreads = kBX * kBY;
 
 DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
@@ -351,7 +356,7 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
-            pp.w[(ii * kTaps + jj) * kThreads] = w;
+            pp.w[(ii * kTaps + jj) * kThreads] = make_float2(w, wr);
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -376,6 +381,11 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
 // v_pk_add: the same IEEE operation per component as the scalar pin).
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// llvm.amdgcn.struct.ptr.buffer.load: the idxen form of buffer_load
+// (address = base + vindex * stride + voffset); clang has no builtin for it.
+__device__ u32x4 amdgcn_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                                                int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
 
 struct ColFetch {
     u32x4 t[kTaps];               // (t00, t01, t10, t11) per sample
@@ -408,8 +418,10 @@ DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFe
         const f2v a = f2v{xs, ys} - fl;
         f.ax[jj] = a.x;
         f.ay[jj] = a.y;
-        const int off = (int)(__umul24((unsigned)((int)fl.y + 1), (unsigned)im.pitch) + (unsigned)((int)fl.x + 1)) * 8;
-        f.t[jj] = __builtin_amdgcn_raw_buffer_load_b128(im.rsrc, off, 0, 0);
+        // record index (y0 + 1) * pitch + x0 + 1 = fma(y0, pitch, x0 + pitch + 1):
+        // integers below 2^24, so exact in fp32 (checked on the host)
+        const unsigned idx = (unsigned)dm_fma(fl.y, im.fpitch, fl.x + im.fp1);
+        f.t[jj] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)idx, 0, 0, 0);
     }
 }
 
@@ -438,7 +450,7 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
     // stays visible and the reads are ds_read, not flat)
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
-    const float *wl = pp.w - pp.wo + wo;
+    const float2 *wl = pp.w - pp.wo + wo;
 #if ACMMP_NCC_PIPELINE
     ColFetch buf[2];
     fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
@@ -459,11 +471,10 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
             const float sv = bilinear_sample(f, jj);
-            const float w = wl[(ii * kTaps + jj) * kThreads];
-            const float wr = w * tile[tb + ii + 2 * kTileW * jj];
-            const float ws = w * sv;
+            const float2 w = wl[(ii * kTaps + jj) * kThreads];
+            const float ws = w.x * sv;
             r_s += ws;
-            racc = fma2(f2v{ws, wr}, f2v{sv, sv}, racc);
+            racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
         }
         sum_src += r_s;
         sum_ss += racc.x;
@@ -721,7 +732,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 template <int NS>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float wlds[kSamples * kThreads];
+    __shared__ float2 wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -812,7 +823,7 @@ template <int NS>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float wlds[kSamples * kThreads];
+    __shared__ float2 wlds[kSamples * kThreads];
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -990,13 +1001,14 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
-    for (int d = 0; d < 8; ++d) {
-        if ((flags >> d) & 1u) {
-            const float4 h = cand(d);
-            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, h);
-        } else {
+    for (int d = 0; d < 8; ++d)
+        if (!((flags >> d) & 1u))
             for (int v = 0; v < nsrc; ++v) cost_array[d][v] = (d == 0 && v == 0) ? 2.0f : 0.0f;
-        }
+    // view-major: the 8 candidates of one source view gather from nearly the
+    // same footprint, back to back, so it stays in L1 (results independent)
+    for (int v = 0; v < nsrc; ++v) {
+        for (int d = 0; d < 8; ++d)
+            if ((flags >> d) & 1u) cost_array[d][v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
     }
 
     DIAG_T(t_phaseA);
@@ -1325,7 +1337,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float wlds[kSamples * kThreads];
+    __shared__ float2 wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1460,7 +1472,7 @@ __global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int 
 __global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ kvp, int colour, float2 *wpair,
                                                     float4 *stats, int P2) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float wlds[kSamples * kThreads];
+    __shared__ float2 wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const BlockXY blk{(int)blockIdx.x, (int)blockIdx.y};
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
@@ -1474,8 +1486,7 @@ __global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ k
     const int my = g.py * kv.Wh + g.k;
     for (int ii = 0; ii < kTaps; ++ii)
         for (int jj = 0; jj < kTaps; ++jj) {
-            const float w = pp.w[(ii * kTaps + jj) * kThreads];
-            wpair[(size_t)(ii * kTaps + jj) * P2 + my] = make_float2(w, w * tile[g.tb + ii + 2 * kTileW * jj]);
+            wpair[(size_t)(ii * kTaps + jj) * P2 + my] = pp.w[(ii * kTaps + jj) * kThreads];
         }
     stats[my] = make_float4(pp.mean, pp.var, pp.inv_wsum, 0.0f);
 }
