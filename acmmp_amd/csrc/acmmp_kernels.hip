@@ -319,6 +319,14 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // the 36 bilateral weights (ComputeBilateralWeight :353-358) and the
 // normalised ref mean / variance — identical for all 14*(N-1) calls of a
 // pixel-iteration, so computed once (same operations, same order).
+// LDS slot of patch sample (column ii, row jj): in the order the gathers
+// visit them (rows outer with ACMMP_NCC_ROWMAJOR), so consecutive reads are
+// adjacent (ds_read2st64 pairs).
+#ifndef ACMMP_NCC_ROWMAJOR
+#define ACMMP_NCC_ROWMAJOR 1
+#endif
+DEV int widx(int ii, int jj) { return ACMMP_NCC_ROWMAJOR ? jj * kTaps + ii : ii * kTaps + jj; }
+
 struct PixPatch {
     float2 *w;       // LDS: (w, w * ref) at [k * kThreads] for sample k of this lane
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
@@ -356,7 +364,7 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
-            pp.w[(ii * kTaps + jj) * kThreads] = make_float2(w, wr);
+            pp.w[widx(ii, jj) * kThreads] = make_float2(w, wr);
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -436,6 +444,86 @@ DEV float bilinear_sample(const ColFetch &f, int jj) {
     return dm_fma(f.ay[jj], tb.y - tb.x, tb.x);
 }
 
+// Row-order gathers: the 6 samples of one patch row (fixed y) of a lane sit
+// in the same one or two cache lines of the row-paired image, so issuing the
+// patch row by row keeps each wave's working set at ~64 lines between reuses
+// (column order touches 6 lines per lane before coming back) — what matters
+// when the hypotheses of neighbouring lanes are incoherent (early
+// iterations). The per-column projection terms are hoisted.
+struct ColTerms {
+    f2v cxy[kTaps];   // (fma(H0, x, H2), fma(H3, x, H5)) per patch column
+    float cz[kTaps];  // fma(H6, x, H8)
+};
+
+template <bool FAST>
+DEV void fetch_row(const SrcImage &im, const float *H, const ColTerms &ct, int py, int jj, ColFetch &f) {
+    const f2v h14 = f2v{H[1], H[4]};
+    const float fw = (float)im.W, fh = (float)im.H;
+    const float y = (float)(py - 5 + 2 * jj);
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        const f2v hxy = fma2(h14, f2v{y, y}, ct.cxy[ii]);
+        const float hz = dm_fma(H[7], y, ct.cz[ii]);
+        const float inv = recip<FAST>(hz);
+        f2v uv = hxy * f2v{inv, inv};
+        uv = (uv + 0.5f) - 0.5f;
+        const float xs = FAST ? __builtin_amdgcn_fmed3f(uv.x, -1.0f, fw) : fminf(fmaxf(uv.x, -1.0f), fw);
+        const float ys = FAST ? __builtin_amdgcn_fmed3f(uv.y, -1.0f, fh) : fminf(fmaxf(uv.y, -1.0f), fh);
+        const f2v fl = f2v{dm_floor(xs), dm_floor(ys)};
+        const f2v a = f2v{xs, ys} - fl;
+        f.ax[ii] = a.x;
+        f.ay[ii] = a.y;
+        const unsigned idx = (unsigned)dm_fma(fl.y, im.fpitch, fl.x + im.fp1);
+        f.t[ii] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)idx, 0, 0, 0);
+    }
+}
+
+template <bool FAST>
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, int wstride, int px, int py,
+                       float &sum_src, float &sum_ss, float &sum_rs) {
+    ColTerms ct;
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        const float x = (float)(px - 5 + 2 * ii);
+        ct.cxy[ii] = fma2(f2v{H[0], H[3]}, f2v{x, x}, f2v{H[2], H[5]});
+        ct.cz[ii] = dm_fma(H[6], x, H[8]);
+    }
+    // per-column partial sums, accumulated row by row: within a column the
+    // rows are still added in order jj = 0..5 (the pinned order,
+    // src/ACMMP.cu:382-412), columns are summed at the end in order ii
+    float r_s[kTaps];
+    f2v racc[kTaps];
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        r_s[ii] = 0.0f;
+        racc[ii] = f2v{0.0f, 0.0f};
+    }
+    // rows are a rolled loop: one row's 6 gathers in flight, reduced, next row
+    // (unrolling lets the compiler hoist every row's address math and spill)
+#pragma unroll 1
+    for (int jj = 0; jj < kTaps; ++jj) {
+        ColFetch f;
+        fetch_row<FAST>(im, H, ct, py, jj, f);
+#pragma unroll
+        for (int ii = 0; ii < kTaps; ++ii) {
+            const float sv = bilinear_sample(f, ii);
+            const float2 w = wl[widx(ii, jj) * wstride];
+            const float ws = w.x * sv;
+            r_s[ii] += ws;
+            racc[ii] = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc[ii]);
+        }
+    }
+    sum_src = 0.0f;
+    sum_ss = 0.0f;
+    sum_rs = 0.0f;
+#pragma unroll
+    for (int ii = 0; ii < kTaps; ++ii) {
+        sum_src += r_s[ii];
+        sum_ss += racc[ii].x;
+        sum_rs += racc[ii].y;
+    }
+}
+
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // software-pipelined one patch column ahead (column ii+1's gathers are in
 // flight while column ii is reduced). Returns the three weighted sums.
@@ -451,6 +539,10 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
     const float2 *wl = pp.w - pp.wo + wo;
+#if ACMMP_NCC_ROWMAJOR
+    ncc_sums_rows<FAST>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
+    return;
+#endif
 #if ACMMP_NCC_PIPELINE
     ColFetch buf[2];
     fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
@@ -471,7 +563,7 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb,
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
             const float sv = bilinear_sample(f, jj);
-            const float2 w = wl[(ii * kTaps + jj) * kThreads];
+            const float2 w = wl[widx(ii, jj) * kThreads];
             const float ws = w.x * sv;
             r_s += ws;
             racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
@@ -1486,7 +1578,7 @@ __global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ k
     const int my = g.py * kv.Wh + g.k;
     for (int ii = 0; ii < kTaps; ++ii)
         for (int jj = 0; jj < kTaps; ++jj) {
-            wpair[(size_t)(ii * kTaps + jj) * P2 + my] = pp.w[(ii * kTaps + jj) * kThreads];
+            wpair[(size_t)widx(ii, jj) * P2 + my] = pp.w[widx(ii, jj) * kThreads];
         }
     stats[my] = make_float4(pp.mean, pp.var, pp.inv_wsum, 0.0f);
 }
@@ -1510,7 +1602,7 @@ DEV void ncc_sums_lean(const SrcImage &im, const float *H, const float2 (*wl)[64
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
             const float sv = bilinear_sample(f, jj);
-            const float2 w = wl[ii * kTaps + jj][lane];
+            const float2 w = wl[widx(ii, jj)][lane];
             const float ws = w.x * sv;
             r_s += ws;
             racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
@@ -1553,7 +1645,8 @@ __global__ __launch_bounds__(576) void k_probe(const KViews *__restrict__ kvp, K
             const float2 pt = project(H, (float)px, (float)py);
             if (!(pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f)) {
                 float sum_src, sum_ss, sum_rs;
-                ncc_sums_lean<true, PIPE>(im, H, wl, lane, px, py, sum_src, sum_ss, sum_rs);
+                if (PIPE == 2) ncc_sums_rows<true>(im, H, &wl[0][lane], 64, px, py, sum_src, sum_ss, sum_rs);
+                else ncc_sums_lean<true, PIPE>(im, H, wl, lane, px, py, sum_src, sum_ss, sum_rs);
                 sum_src *= ps.z;
                 sum_ss *= ps.z;
                 sum_rs *= ps.z;
@@ -1584,15 +1677,14 @@ int probe_run(const KViews *d_kv, const KViews &h_kv, const KState &st, int vari
     hipEventCreate(&a);
     hipEventCreate(&b);
     dim3 grid((h_kv.Wh + 63) / 64, h_kv.H), block(64, 9);
-    for (int w = 0; w < 2; ++w) {
+    auto launch = [&]() {
         if (variant == 0) k_probe<0><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-        else k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-    }
+        else if (variant == 1) k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+        else k_probe<2><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
+    };
+    for (int w = 0; w < 2; ++w) launch();
     hipEventRecord(a, s);
-    for (int r = 0; r < reps; ++r) {
-        if (variant == 0) k_probe<0><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-        else k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-    }
+    for (int r = 0; r < reps; ++r) launch();
     hipEventRecord(b, s);
     hipEventSynchronize(b);
     hipEventElapsedTime(ms, a, b);

@@ -1,4 +1,7 @@
-"""Split-kernel NCC throughput probe (diagnostic; ACMMP_DIAG_PROBE build).
+"""Split-kernel NCC throughput probe (diagnostic; ACMMP_DIAG_PROBE build):
+lean one-thread-per-(pixel, candidate) kernel, variants 0/1 = column-order
+gathers (plain / pipelined), 2 = row-order gathers; on random (init-only)
+and on converged (8-iteration) hypotheses.
 usage: ACMMP_LIB=acmmp_amd/lib/variants/libacmmp_amd_probe.so python tools/probe_ncc.py"""
 import ctypes as C
 import os
@@ -15,17 +18,17 @@ dev = torch.device("cuda", 0)
 setup = scene.scene_setup(num_views=10, width=1600, height=1200)
 ids = [0] + setup.pairs[0][:9]
 imgs = [scene.render_torch(setup, i, dev) for i in ids]
-eng = ACMMP(0)
-p = default_params()
-p.max_iterations = 8
-eng.set_params(p)
-eng.set_timing(True)
-eng.set_images_device([setup.camera(i) for i in ids], [im.data_ptr() for im in imgs])
-eng.RunPatchMatch()
-eng.RunPatchMatch()
-t = eng.timing()
-print("k_sweep ms/launch", t["sweep_ms"] / t["sweep_launches"])
-for variant in (0, 1):
-    ms = C.c_float(0)
-    rc = fn(eng._ctx, variant, 5, C.byref(ms))
-    print("probe variant", variant, "rc", rc, "ms", ms.value, "per 960k-NCC-pass us", 1000 * ms.value / 81)
+for iters in (0, 8):
+    eng = ACMMP(0)
+    p = default_params()
+    p.max_iterations = iters
+    eng.set_params(p)
+    eng.set_timing(True)
+    eng.set_images_device([setup.camera(i) for i in ids], [im.data_ptr() for im in imgs])
+    eng.RunPatchMatch()
+    for variant in (0, 1, 2):
+        ms = C.c_float(0)
+        rc = fn(eng._ctx, variant, 5, C.byref(ms))
+        print(f"state after {iters} iters: variant {variant} rc {rc} ms {ms.value:.3f} "
+              f"per 960k-NCC-pass us {1000 * ms.value / 81:.1f}", flush=True)
+    eng.close()
