@@ -20,6 +20,8 @@
 #include <string>
 #include <vector>
 
+#include <zlib.h>
+
 #include "../../include/acmmp.h"
 
 namespace {
@@ -529,6 +531,81 @@ int decode_any(const char *path, bool size_only, int &W, int &H, std::vector<flo
     return ACMMP_ERR_UNSUPPORTED;
 }
 
+// ------------------------------------------------------------------ PNG
+// cv::imread(path, IMREAD_UNCHANGED) of the non-interlaced 8/16-bit gray /
+// RGB / RGBA PNGs the seeded-prior loader reads (src/acmmp_definitions.cpp:
+// 104-106): samples as stored (16-bit big-endian -> host), colour channels
+// reordered to OpenCV's BGR(A).
+uint32_t be32(const uint8_t *q) { return (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3]; }
+
+int png_decode(const std::vector<uint8_t> &b, int &W, int &H, int &C, int &depth, std::vector<uint16_t> *out) {
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    if (b.size() < 8 || std::memcmp(b.data(), sig, 8) != 0) return ACMMP_ERR_IO;
+    size_t o = 8;
+    int ctype = -1, interlace = 0;
+    std::vector<uint8_t> z;
+    while (o + 12 <= b.size()) {
+        const uint32_t len = be32(&b[o]);
+        if (o + 12 + (size_t)len > b.size()) return ACMMP_ERR_IO;
+        const uint8_t *type = &b[o + 4], *d = &b[o + 8];
+        if (!std::memcmp(type, "IHDR", 4)) {
+            if (len < 13) return ACMMP_ERR_IO;
+            W = (int)be32(d);
+            H = (int)be32(d + 4);
+            depth = d[8];
+            ctype = d[9];
+            interlace = d[12];
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            z.insert(z.end(), d, d + len);
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        o += 12 + len;
+    }
+    if (ctype < 0 || W <= 0 || H <= 0) return ACMMP_ERR_IO;
+    if (interlace || (depth != 8 && depth != 16)) return ACMMP_ERR_UNSUPPORTED;
+    C = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
+    if (C == 0) return ACMMP_ERR_UNSUPPORTED;  // palette
+    if (!out) return ACMMP_OK;
+    const size_t bpp = (size_t)C * depth / 8, stride = bpp * W;
+    std::vector<uint8_t> raw((stride + 1) * H);
+    uLongf rawlen = (uLongf)raw.size();
+    if (uncompress(raw.data(), &rawlen, z.data(), (uLong)z.size()) != Z_OK || rawlen != raw.size())
+        return ACMMP_ERR_IO;
+    std::vector<uint8_t> prev(stride, 0), cur(stride);
+    out->resize((size_t)W * H * C);
+    for (int y = 0; y < H; ++y) {
+        const uint8_t f = raw[(stride + 1) * y];
+        const uint8_t *src = &raw[(stride + 1) * y + 1];
+        for (size_t i = 0; i < stride; ++i) {
+            const int a = i >= bpp ? cur[i - bpp] : 0, up = prev[i], c = i >= bpp ? prev[i - bpp] : 0;
+            int v = src[i];
+            switch (f) {
+                case 0: break;
+                case 1: v += a; break;
+                case 2: v += up; break;
+                case 3: v += (a + up) >> 1; break;
+                case 4: {
+                    const int p0 = a + up - c, pa = std::abs(p0 - a), pb = std::abs(p0 - up), pc = std::abs(p0 - c);
+                    v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? up : c);
+                    break;
+                }
+                default: return ACMMP_ERR_IO;
+            }
+            cur[i] = (uint8_t)v;
+        }
+        for (int x = 0; x < W; ++x)
+            for (int k = 0; k < C; ++k) {
+                // RGB(A) -> BGR(A), as cv::imread
+                const int sk = (C >= 3 && k < 3) ? 2 - k : k;
+                const size_t si = ((size_t)x * C + sk) * (depth / 8);
+                (*out)[((size_t)y * W + x) * C + k] = depth == 16 ? (uint16_t)(cur[si] << 8 | cur[si + 1]) : cur[si];
+            }
+        prev.swap(cur);
+    }
+    return ACMMP_OK;
+}
+
 // ------------------------------------------------------------- resize
 // cv::resize(src, dst, Size(nw, nh), 0, 0, INTER_LINEAR) for CV_32FC1: the
 // exact-2x downscale takes OpenCV's INTER_AREA fast path (2x2 mean), other
@@ -611,6 +688,26 @@ int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *wi
     *height = H;
     if (!out || capacity < img.size()) return ACMMP_ERR_ARG;
     std::memcpy(out, img.data(), img.size() * sizeof(float));
+    return ACMMP_OK;
+}
+
+int acmmp_read_png(const char *path, uint16_t *out, size_t capacity, int *width, int *height, int *channels,
+                   int *bit_depth) {
+    if (!width || !height || !channels) return ACMMP_ERR_ARG;
+    std::vector<uint8_t> buf;
+    if (!path || !read_file(path, buf)) return ACMMP_ERR_IO;
+    int W = 0, H = 0, C = 0, depth = 0;
+    int rc = png_decode(buf, W, H, C, depth, nullptr);
+    if (rc) return rc;
+    *width = W;
+    *height = H;
+    *channels = C;
+    if (bit_depth) *bit_depth = depth;
+    if (!out || capacity < (size_t)W * H * C) return ACMMP_ERR_ARG;
+    std::vector<uint16_t> px;
+    rc = png_decode(buf, W, H, C, depth, &px);
+    if (rc) return rc;
+    std::memcpy(out, px.data(), px.size() * sizeof(uint16_t));
     return ACMMP_OK;
 }
 

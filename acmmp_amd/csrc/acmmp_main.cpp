@@ -24,7 +24,7 @@ void usage() {
     std::printf(
         "usage: acmmp_main <dense_folder> [options]\n"
         "  --output_dir NAME        output working directory name (default /ACMMP)\n"
-        "  -p, --prior              run from a provided prior (not supported)\n"
+        "  -p, --prior              seed the first pass from <dense>priors/{depths,normals}/NNNNNNNN.png\n"
         "  --device N               HIP device (default 0)\n"
         "  --iterations N           PatchMatch iterations per run (default: the reference's 2)\n"
         "  --seed N                 base RNG seed (default 1234)\n"
@@ -43,7 +43,7 @@ int die(const char *what) {
 
 int main(int argc, char **argv) {
     std::string dense_folder, output_dir = "/ACMMP";
-    bool prior = false, quiet = false, triangulation = true;
+    bool prior = false, quiet = false, triangulation = true, renamed_outdir = false;
     int device = 0, iterations = 0;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
@@ -62,6 +62,7 @@ int main(int argc, char **argv) {
             prior = true;
         } else if (a == "--output_dir") {
             output_dir = value();
+            renamed_outdir = true;
         } else if (a == "--device") {
             device = std::atoi(value().c_str());
         } else if (a == "--iterations") {
@@ -90,10 +91,6 @@ int main(int argc, char **argv) {
         usage();
         return 2;
     }
-    if (prior) {
-        std::fprintf(stderr, "acmmp_main: initialisation from a prior (-p) is not supported by this build\n");
-        return 1;
-    }
 
     std::vector<acmmp_problem> problems(4096);
     int num_images = 0;
@@ -104,6 +101,13 @@ int main(int argc, char **argv) {
     int max_num_downscale = -1;
     if (acmmp_compute_multiscale_settings(dense_folder.c_str(), problems.data(), num_images, &max_num_downscale))
         return die("ComputeMultiScaleSettings");
+    // pSampler (src/main_ACMMP.cpp:72-90): priors must exist; default output
+    // folder name changes unless --output_dir was given
+    if (prior && !acmmp_priors_available(dense_folder.c_str(), num_images)) {
+        std::printf("Initialisation from a prior was requested, but no suitable priors were found.\n");
+        return -1;
+    }
+    if (prior && !renamed_outdir) output_dir = "/ACMMP_PRIOR";
     const std::string output_folder = dense_folder + output_dir;
     ::mkdir(output_folder.c_str(), 0777);
 
@@ -114,7 +118,8 @@ int main(int argc, char **argv) {
     opt.write_triangulation = triangulation ? 1 : 0;
     opt.verbose = quiet ? 0 : 1;
     unsigned pass = 0;
-    auto run_pass = [&](bool geom, bool planar, bool hier, bool multi) -> bool {
+    auto run_pass = [&](bool geom, bool planar, bool hier, bool multi, bool seeded = false) -> bool {
+        opt.seeded = seeded;
         opt.geom_consistency = geom;
         opt.planar_prior = planar;
         opt.hierarchy = hier;
@@ -141,7 +146,7 @@ int main(int argc, char **argv) {
         }
         if (flag == 0) {
             flag = 1;
-            if (!run_pass(false, true, false, false)) return die("ProcessProblem");
+            if (!run_pass(false, true, false, false, prior)) return die("ProcessProblem");
         } else {
             if (!quiet) std::printf("Starting JBU\n");
             for (auto &p : problems)

@@ -207,9 +207,88 @@ int load_view(const std::string &dense, int id, int max_image_size, acmmp::Image
     return ACMMP_OK;
 }
 
+// ---- pSampler (src/acmmp_definitions.cpp:8-177): seeded plane priors from
+// 16-bit PNG depth / normal maps under <dense>priors/{depths,normals}/%08d.png
+// (the reference concatenates "priors" to dense_folder without a separator).
+std::string prior_path(const std::string &dense, const char *kind, int cam) {
+    return dense + "priors/" + kind + "/" + id8(cam) + ".png";
+}
+
+bool read_png(const std::string &path, std::vector<uint16_t> &px, int &w, int &h, int &c) {
+    int bd = 0;
+    if (acmmp_read_png(path.c_str(), nullptr, 0, &w, &h, &c, &bd) != ACMMP_ERR_ARG) return false;
+    px.resize((size_t)w * h * c);
+    return acmmp_read_png(path.c_str(), px.data(), px.size(), &w, &h, &c, &bd) == ACMMP_OK;
+}
+
+// depth_normal_to_plane (:72-89) with getViewDirection, normVec3 (which
+// multiplies by the norm instead of dividing: kept) and distance_to_origin.
+void depth_normal_to_plane(float depth, float nx, float ny, float nz, int px, int py, const acmmp_camera &cam,
+                           float *out) {
+    const float X0 = depth * (px - cam.K[2]) / cam.K[0];
+    const float X1 = depth * (py - cam.K[5]) / cam.K[4];
+    const float X2 = depth;
+    const float norm = std::sqrt(X0 * X0 + X1 * X1 + X2 * X2);
+    const float v0 = X0 / norm, v1 = X1 / norm, v2 = X2 / norm;
+    const float dot = nx * v0 + ny * v1 + nz * v2;
+    if (dot > 0.0f) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    const float n2 = nx * nx + ny * ny + nz * nz;
+    const float s = std::sqrt(n2);
+    nx *= s;
+    ny *= s;
+    nz *= s;
+    out[0] = nx;
+    out[1] = ny;
+    out[2] = nz;
+    out[3] = -(nx * X0 + ny * X1 + nz * X2);
+}
+
 }  // namespace
 
 extern "C" {
+
+int acmmp_priors_available(const char *dense_folder, int num_cams) {
+    if (!dense_folder || num_cams <= 0) return 0;
+    std::vector<uint16_t> px;
+    int w, h, c;
+    return read_png(prior_path(dense_folder, "depths", num_cams - 1), px, w, h, c) &&
+           read_png(prior_path(dense_folder, "normals", num_cams - 1), px, w, h, c);
+}
+
+int acmmp_prior_plane_estimate(const char *dense_folder, int cam_num, const acmmp_camera *cam, int rows, int cols,
+                               float *planes4) {
+    if (!dense_folder || !cam || rows <= 0 || cols <= 0 || !planes4) return fail(ACMMP_ERR_ARG, "bad args");
+    std::vector<uint16_t> dpx, npx;
+    int dw, dh, dc, nw, nh, nc;
+    const std::string dp = prior_path(dense_folder, "depths", cam_num), np = prior_path(dense_folder, "normals", cam_num);
+    if (!read_png(dp, dpx, dw, dh, dc) || !read_png(np, npx, nw, nh, nc))
+        return fail(ACMMP_ERR_IO, "failed to load prior images: %d (%s)", cam_num, dp.c_str());
+    if (nc != 3) return fail(ACMMP_ERR_UNSUPPORTED, "prior normal map %s has %d channels", np.c_str(), nc);
+    // Mat::convertTo(CV_32F, alpha, beta): src * alpha + beta in float
+    const float dist = cam->depth_max - cam->depth_min;
+    const float range = dist / 65535.0f;
+    const float nalpha = (float)(2.0 / 65536.0), nbeta = -1.0f;
+    const int scale = dh / rows;  // src/acmmp_definitions.cpp:126
+    for (int i = 0; i < rows; ++i)
+        for (int j = 0; j < cols; ++j) {
+            const int r = i * scale, c = j * scale;
+            // Mat_<float>::at(r, c) on the (possibly multi-channel) depth map
+            const size_t di = (size_t)r * dw * dc + c;
+            const size_t ni = ((size_t)r * nw + c) * 3;
+            if (r >= dh || di >= dpx.size() || r >= nh || c >= nw)
+                return fail(ACMMP_ERR_ARG, "prior maps %dx%d smaller than %dx%d", dw, dh, cols, rows);
+            const float base_d = (float)dpx[di] * range + cam->depth_min;
+            const float nx = (float)npx[ni] * nalpha + nbeta;
+            const float ny = (float)npx[ni + 1] * nalpha + nbeta;
+            const float nz = (float)npx[ni + 2] * nalpha + nbeta;
+            depth_normal_to_plane(base_d, nx, ny, nz, j, i, *cam, planes4 + ((size_t)i * cols + j) * 4);
+        }
+    return ACMMP_OK;
+}
 
 int acmmp_load_view(const char *dense_folder, int image_id, int max_image_size, float *out, size_t capacity,
                     acmmp_camera *cam) {
@@ -386,7 +465,6 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
                           int count, int idx, const acmmp_pass_options *opt) {
     if (!dense_folder || !output_folder || !problems || !opt || idx < 0 || idx >= count)
         return fail(ACMMP_ERR_ARG, "bad args");
-    if (opt->seeded) return fail(ACMMP_ERR_UNSUPPORTED, "seeded priors (pSampler) are not supported");
     const acmmp_problem &problem = problems[idx];
     if (opt->verbose) std::printf("Processing image %s...\n", id8(problem.ref_image_id).c_str());
     const std::string folder = result_folder(output_folder, problem.ref_image_id);
@@ -404,6 +482,14 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
         acmmp.InputInitialization(dense_folder, output_folder, all, idx);
         acmmp.CudaSpaceInitialization(output_folder, problem);
         const int width = acmmp.GetReferenceImageWidth(), height = acmmp.GetReferenceImageHeight();
+        if (opt->seeded) {  // :275-281; GetCamera(idx) indexes this problem's cameras with the problem index
+            const acmmp_params prm = acmmp.params();
+            const acmmp::Camera cam = acmmp.GetCamera(idx < prm.num_images ? idx : 0);
+            std::vector<acmmp::Float4> prior((size_t)width * height);
+            const int rc = acmmp_prior_plane_estimate(dense_folder, idx, &cam, height, width, &prior[0].x);
+            if (rc) return rc;
+            acmmp.SetPlanarPrior(prior);
+        }
         acmmp.RunPatchMatch();
         if (opt->planar_prior) {  // :301-379
             if (opt->verbose) std::printf("Run Planar Prior Assisted PatchMatch MVS ...\n");

@@ -56,10 +56,27 @@ def compute_multiscale_settings(dense_folder: str, problems: list) -> int:
     return k.value
 
 
+def priors_available(dense_folder: str, num_cams: int) -> bool:
+    """pSampler::confirm_using_prior (src/acmmp_definitions.cpp:8-29, 91-93)."""
+    return bool(_abi.load_library().acmmp_priors_available(dense_folder.encode(), num_cams))
+
+
+def prior_plane_estimate(dense_folder: str, cam_num: int, cam, rows: int, cols: int):
+    """pSampler::GetPriorPlaneEstimate (src/acmmp_definitions.cpp:99-177)."""
+    import numpy as np
+    out = np.empty((rows, cols, 4), dtype=np.float32)
+    rc = _abi.load_library().acmmp_prior_plane_estimate(dense_folder.encode(), cam_num, C.byref(cam), rows, cols,
+                                                        out.ctypes.data_as(C.POINTER(C.c_float)))
+    if rc != 0:
+        _err("GetPriorPlaneEstimate", rc)
+    return out
+
+
 def pass_options(geom_consistency=False, planar_prior=False, hierarchy=False, multi_geometry=False,
                  device=0, max_iterations=0, seed_lo=1234, seed_hi=0, write_triangulation=True,
-                 verbose=False) -> _abi.PassOptions:
+                 verbose=False, seeded=False) -> _abi.PassOptions:
     o = _abi.PassOptions()
+    o.seeded = int(seeded)
     o.device = device
     o.geom_consistency = int(geom_consistency)
     o.planar_prior = int(planar_prior)
@@ -101,20 +118,25 @@ def scale_step(problems: list) -> None:
             p.num_downscale -= 1
 
 
-def run_sequential(dense_folder: str, output_dir: str = "/ACMMP", device: int = 0, max_iterations: int = 0,
+def run_sequential(dense_folder: str, output_dir: str | None = None, device: int = 0, max_iterations: int = 0,
                    seed: int = 1234, write_triangulation: bool = True, geom_iterations: int = 2,
-                   verbose: bool = False) -> str:
-    """main_ACMMP's multi-scale loop without fusion; returns the output folder."""
+                   verbose: bool = False, prior: bool = False) -> str:
+    """main_ACMMP's multi-scale loop without fusion; returns the output folder.
+    prior=True is the -p flag: seeded first pass, default folder /ACMMP_PRIOR."""
     problems = generate_sample_list(dense_folder)
     max_num_downscale = compute_multiscale_settings(dense_folder, problems)
+    if prior and not priors_available(dense_folder, len(problems)):
+        raise AcmmpError("Initialisation from a prior was requested, but no suitable priors were found.")
+    if output_dir is None:
+        output_dir = "/ACMMP_PRIOR" if prior else "/ACMMP"
     output_folder = dense_folder + output_dir
     os.makedirs(output_folder, exist_ok=True)
     state = {"pass": 0}
 
-    def run_pass(geom, planar, hier, multi):
+    def run_pass(geom, planar, hier, multi, seeded=False):
         for i, p in enumerate(problems):
             opt = pass_options(geom, planar, hier, multi, device, max_iterations, seed + p.ref_image_id,
-                               state["pass"], write_triangulation, verbose)
+                               state["pass"], write_triangulation, verbose, seeded)
             process_problem(dense_folder, output_folder, problems, i, opt)
         state["pass"] += 1
 
@@ -123,7 +145,7 @@ def run_sequential(dense_folder: str, output_dir: str = "/ACMMP", device: int = 
         scale_step(problems)
         if first:
             first = False
-            run_pass(False, True, False, False)
+            run_pass(False, True, False, False, prior)
         else:
             for p in problems:
                 joint_bilateral_upsampling(dense_folder, output_folder, p, p.cur_image_size, device)

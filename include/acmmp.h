@@ -331,6 +331,19 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
  * 2333_%08d/depths.dmb. */
 int acmmp_joint_bilateral_upsampling(const char *dense_folder, const char *output_folder,
                                      const acmmp_problem *problem, int acmmp_size, int device);
+/* ~ pSampler::pSampler / confirm_using_prior (src/acmmp_definitions.cpp:8-29,
+ * 91-93): 1 when <dense>priors/{depths,normals}/%08d.png of camera
+ * num_cams-1 can be read (the path is dense_folder + "priors", as in the
+ * reference), else 0. */
+int acmmp_priors_available(const char *dense_folder, int num_cams);
+/* ~ pSampler::GetPriorPlaneEstimate (src/acmmp_definitions.cpp:99-177): the
+ * seeded plane prior of camera `cam_num` at rows x cols from the 16-bit depth
+ * (mapped to [cam.depth_min, depth_max]) and normal (mapped to [-1, 1], BGR)
+ * PNGs, through depth_normal_to_plane (:72-89) — including normVec3's
+ * multiplication by the norm. float4 per pixel, row-major. */
+int acmmp_prior_plane_estimate(const char *dense_folder, int cam_num, const acmmp_camera *cam, int rows, int cols,
+                               float *planes4);
+
 /* Message of the last failing driver call on this thread ("" when none). */
 const char *acmmp_pipeline_last_error(void);
 
@@ -355,6 +368,12 @@ int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *wi
 /* Image dimensions from the file header only (ComputeMultiScaleSettings,
  * src/acmmp_definitions.cpp:219-224, decodes the whole image for this). */
 int acmmp_image_size(const char *path, int *width, int *height);
+/* ~ cv::imread(path, IMREAD_UNCHANGED) of a non-interlaced 8/16-bit gray,
+ * gray+alpha, RGB or RGBA PNG: samples widened to uint16, colour channels in
+ * OpenCV's BGR(A) order. Writes width*height*channels values when capacity
+ * suffices; otherwise ACMMP_ERR_ARG with the dimensions set. */
+int acmmp_read_png(const char *path, uint16_t *out, size_t capacity, int *width, int *height, int *channels,
+                   int *bit_depth);
 /* ~ cv::resize(src, dst, Size(dst_width, dst_height), 0, 0, INTER_LINEAR) on
  * a float image (src/ACMMP.cpp:589): half-pixel centres, edge clamp,
  * horizontal pass first; an exact 2x downscale is the 2x2 mean (OpenCV's

@@ -123,3 +123,48 @@ void acmmp_oracle_planar_prior(const acmmp_camera *cam, const float *depths, int
     }
     free(mask_tri);
 }
+
+/* pSampler::GetPriorPlaneEstimate (src/acmmp_definitions.cpp:99-177) on
+ * already-decoded 16-bit maps: depth (dh x dw x dc, interleaved) and normals
+ * (nh x nw x 3, BGR as cv::imread returns them). Mat::convertTo(alpha, beta)
+ * is src * alpha + beta in float; depth_normal_to_plane (:72-89) keeps
+ * normVec3's multiplication by the norm (:34-41). */
+void acmmp_oracle_prior_plane_estimate(const uint16_t *depth, int dw, int dh, int dc, const uint16_t *normals,
+                                       int nw, const acmmp_camera *cam, int rows, int cols, float *planes4) {
+    const float dist = cam->depth_max - cam->depth_min;
+    const float range = dist / 65535.0f;
+    const float alpha = (float)(2.0 / 65536.0), beta = -1.0f;
+    const int scale = dh / rows;
+    for (int i = 0; i < rows; i++) {
+        for (int j = 0; j < cols; ++j) {
+            const int k = i * cols + j;
+            const float base_d = (float)depth[(size_t)(i * scale) * dw * dc + (size_t)(j * scale)] * range +
+                                 cam->depth_min;
+            const uint16_t *nv = normals + ((size_t)(i * scale) * nw + (size_t)(j * scale)) * 3;
+            float n[4] = {(float)nv[0] * alpha + beta, (float)nv[1] * alpha + beta, (float)nv[2] * alpha + beta,
+                          0.0f};
+            /* getViewDirection */
+            float X[3];
+            X[0] = base_d * (j - cam->K[2]) / cam->K[0];
+            X[1] = base_d * (i - cam->K[5]) / cam->K[4];
+            X[2] = base_d;
+            const float norm = sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+            const float vd[3] = {X[0] / norm, X[1] / norm, X[2] / norm};
+            const float dot_product = n[0] * vd[0] + n[1] * vd[1] + n[2] * vd[2];
+            if (dot_product > 0.0f) {
+                n[0] = -n[0];
+                n[1] = -n[1];
+                n[2] = -n[2];
+            }
+            /* normVec3 */
+            const float normSquared = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+            const float inverse_sqrt = sqrtf(normSquared);
+            n[0] *= inverse_sqrt;
+            n[1] *= inverse_sqrt;
+            n[2] *= inverse_sqrt;
+            /* distance_to_origin */
+            n[3] = -(n[0] * X[0] + n[1] * X[1] + n[2] * X[2]);
+            memcpy(planes4 + 4 * (size_t)k, n, sizeof(n));
+        }
+    }
+}

@@ -68,6 +68,9 @@ def _load():
     lib.acmmp_oracle_planar_prior.restype = None
     lib.acmmp_oracle_planar_prior.argtypes = [CAM, FP, C.c_int, C.c_int, C.c_float, C.c_float, I32P, C.c_int,
                                               FP, U32P, FP]
+    lib.acmmp_oracle_prior_plane_estimate.restype = None
+    lib.acmmp_oracle_prior_plane_estimate.argtypes = [C.POINTER(C.c_uint16), C.c_int, C.c_int, C.c_int,
+                                                      C.POINTER(C.c_uint16), C.c_int, CAM, C.c_int, C.c_int, FP]
     lib.acmmp_oracle_jbu.restype = C.c_int
     lib.acmmp_oracle_jbu.argtypes = [FP, C.c_int, C.c_int, FP, C.c_int, C.c_int, FP]
     _lib = lib
@@ -233,3 +236,18 @@ def jbu(image, depth):
     out = np.zeros_like(im)
     isc = lib.acmmp_oracle_jbu(_f(im), im.shape[1], im.shape[0], _f(d), d.shape[1], d.shape[0], _f(out))
     return (None if isc == 1 else out), isc
+
+
+def prior_plane_estimate(depth_u16, normals_bgr_u16, cam, rows, cols):
+    """pSampler::GetPriorPlaneEstimate (src/acmmp_definitions.cpp:99-177) on
+    decoded maps: depth (H, W[, C]) uint16, normals (H, W, 3) uint16 in BGR."""
+    lib = _load()
+    d = np.ascontiguousarray(depth_u16, dtype=np.uint16)
+    n = np.ascontiguousarray(normals_bgr_u16, dtype=np.uint16)
+    dh, dw = d.shape[:2]
+    dc = 1 if d.ndim == 2 else d.shape[2]
+    out = np.zeros((rows, cols, 4), np.float32)
+    u16 = C.POINTER(C.c_uint16)
+    lib.acmmp_oracle_prior_plane_estimate(d.ctypes.data_as(u16), dw, dh, dc, n.ctypes.data_as(u16), n.shape[1],
+                                          C.byref(cam), rows, cols, _f(out))
+    return out

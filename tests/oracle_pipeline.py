@@ -109,13 +109,19 @@ class OraclePipeline:
         for i in self.full_images:
             self.images[i], self.cams[i] = rescale(self.full_images[i], self.full_cams[i], cur_sizes[i])
 
-    def process_problem(self, idx, geom, planar, multi, seed_hi, maps_in, hier=False):
+    def process_problem(self, idx, geom, planar, multi, seed_hi, maps_in, hier=False, seeded=False):
         pr = self.problems[idx]
         ids = [pr.ref_image_id] + list(pr.src_image_ids)
         cams = [self.cams[i] for i in ids]
         imgs = [self.images[i] for i in ids]
         p = _params(cams[0], len(ids), geom, multi, self.seed + pr.ref_image_id, seed_hi)
         kw = {}
+        if seeded:  # pSampler + SetPlanarPrior (src/acmmp_definitions.cpp:275-281)
+            depth_u16, normals_bgr = self.priors[idx]
+            cam = cams[idx] if idx < len(cams) else cams[0]  # GetCamera(idx), as the reference
+            H, W = imgs[0].shape
+            kw["seed_planes"] = oracle.prior_plane_estimate(depth_u16, normals_bgr, cam, H, W)
+            p.seeded = 1
         if hier:  # CudaSpaceInitialization hierarchy branch (src/ACMMP.cpp:745-808)
             ref = pr.ref_image_id
             H, W = imgs[0].shape
@@ -147,7 +153,7 @@ class OraclePipeline:
             _, mask, prior = oracle.planar_prior(cams[0], out["planes"][..., 3], p.depth_min, p.depth_max, tris)
             p.planar_prior = 1
             p.rng_stream = 1
-            extra = {}
+            extra = {"seed_planes": kw["seed_planes"]} if seeded else {}
             if hier:
                 extra = {"pre_costs": out["pre_costs"], "scaled_planes": kw["scaled_planes"]}
             out = oracle.run_patchmatch(p, cams, imgs, planes=out["planes"], costs=out["costs"],
@@ -156,16 +162,19 @@ class OraclePipeline:
         res["depths_geom" if geom else "depths"] = out["planes"][..., 3].copy()
         return res
 
-    def run_pass(self, geom, planar, multi, seed_hi, order="sequential", hier=False):
+    def run_pass(self, geom, planar, multi, seed_hi, order="sequential", hier=False, seeded=False):
         snapshot = dict(self.maps)
         for idx, pr in enumerate(self.problems):
             src = self.maps if order == "sequential" else snapshot
-            res = self.process_problem(idx, geom, planar, multi, seed_hi, src, hier)
+            res = self.process_problem(idx, geom, planar, multi, seed_hi, src, hier, seeded)
             for k, v in res.items():
                 self.maps[(pr.ref_image_id, k)] = v
 
-    def run_single_scale(self, order="sequential", geom_iterations=2):
-        self.run_pass(False, True, False, 0, order)
+    def run_single_scale(self, order="sequential", geom_iterations=2, priors=None):
+        """priors: {problem index: (depth uint16, normals uint16 BGR)} seeds the
+        first pass (main_ACMMP -p)."""
+        self.priors = priors
+        self.run_pass(False, True, False, 0, order, seeded=priors is not None)
         for g in range(geom_iterations):
             self.run_pass(True, False, g > 0, 1 + g, order)
         return self.maps

@@ -69,3 +69,24 @@ def test_multi_scale_jbu_hierarchy_matches_oracle(tmp_path):
     maps = OraclePipeline(d).run_multi_scale("sequential")
     assert _compare(out, maps) == 3 * 4
     assert aio.read_dmb(os.path.join(aio.result_folder(out, 0), "depths_geom.dmb")).shape == (760, 1010)
+
+
+def test_seeded_pipeline_matches_oracle(tmp_path):
+    """main_ACMMP -p: the first pass is seeded from 16-bit prior PNGs
+    (pSampler, src/acmmp_definitions.cpp:99-177, SetPlanarPrior)."""
+    from test_seeded_priors import _write_priors
+    d = str(tmp_path / "dense") + "/"
+    sc = scene.make_scene(num_views=4, width=128, height=96)
+    scene.write_dense_folder(sc, d, num_src=3)
+    rng = np.random.default_rng(5)
+    priors = {}
+    for i, v in enumerate(sc.views):
+        dep = np.clip((v.depth - 300.0) / 500.0 * 65535.0 + rng.normal(0, 300, v.depth.shape), 0, 65535)
+        dep = np.where(v.depth > 0, dep, 30000).astype(np.uint16)
+        nrm = np.clip((v.normal + 1.0) * 32768.0, 0, 65535).astype(np.uint16)
+        _write_priors(d, i, dep, nrm)
+        priors[i] = (dep, nrm[..., ::-1])
+    out = pipeline.run_sequential(d, prior=True, write_triangulation=False)
+    assert out.endswith("/ACMMP_PRIOR")
+    maps = OraclePipeline(d).run_single_scale("sequential", priors=priors)
+    assert _compare(out, maps) == 4 * 4
