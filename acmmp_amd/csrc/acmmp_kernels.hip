@@ -1093,51 +1093,52 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
-    for (int d = 0; d < 8; ++d)
-        if (!((flags >> d) & 1u))
-            for (int v = 0; v < nsrc; ++v) cost_array[d][v] = (d == 0 && v == 0) ? 2.0f : 0.0f;
-    // view-major: the 8 candidates of one source view gather from nearly the
-    // same footprint, back to back, so it stays in L1 (results independent)
-    for (int v = 0; v < nsrc; ++v) {
-        for (int d = 0; d < 8; ++d)
-            if ((flags >> d) & 1u) cost_array[d][v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
-    }
-
-    DIAG_T(t_phaseA);
-    // ---- multi-hypothesis joint view selection (:994-1056)
+    // view-selection inputs (:994-1032), folded into the view-major candidate
+    // loop so each view's 8 costs are consumed from registers
     float probs[NS];
+    uint32_t nb[4];
     {
         const uint32_t *sv_opp = st.sv[oc];
-        const int kc = g.k;
-        uint32_t nb[4];
         // (x, y+-1) are colour-split column (x >> 1); (x+-1, y) are k - 1 + s, k + s
         nb[0] = (py > 0) ? sv_opp[(py - 1) * Wh + (px >> 1)] : 0u;
         nb[1] = (py < height - 1) ? sv_opp[(py + 1) * Wh + (px >> 1)] : 0u;
         nb[2] = (px > 0) ? sv_opp[py * Wh + ((px - 1) >> 1)] : 0u;
         nb[3] = (px < width - 1) ? sv_opp[py * Wh + ((px + 1) >> 1)] : 0u;
-        (void)kc;
-        const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
-        for (int i = 0; i < nsrc; i++) {
-            float vsp = 0.0f;
-            for (int n = 0; n < 4; ++n)
-                if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> i) & 1u) ? 0.9f : 0.1f;
-            float count = 0;
-            int count_false = 0;
-            float tmpw = 0;
-            for (int j = 0; j < 8; j++) {
-                const float c = cost_array[j][i];
-                if (c < cost_threshold) {
-                    tmpw += dm_expf(c * c / (-0.18f));
-                    count++;
-                }
-                if (c > 1.2f) count_false++;
-            }
-            float pr = 0.0f;
-            if (count > 2 && count_false < 3) pr = tmpw / count;
-            else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
-            probs[i] = pr * vsp;
-        }
     }
+    const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
+    // view-major: the 8 candidates of one source view gather from nearly the
+    // same footprint, back to back (results are independent)
+    for (int v = 0; v < nsrc; ++v) {
+        float cv[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            if ((flags >> d) & 1u) cv[d] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
+            else cv[d] = (d == 0 && v == 0) ? 2.0f : 0.0f;
+            cost_array[d][v] = cv[d];
+        }
+        float vsp = 0.0f;
+        for (int n = 0; n < 4; ++n)
+            if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> v) & 1u) ? 0.9f : 0.1f;
+        float count = 0;
+        int count_false = 0;
+        float tmpw = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float c = cv[j];
+            if (c < cost_threshold) {
+                tmpw += dm_expf(c * c / (-0.18f));
+                count++;
+            }
+            if (c > 1.2f) count_false++;
+        }
+        float pr = 0.0f;
+        if (count > 2 && count_false < 3) pr = tmpw / count;
+        else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
+        probs[v] = pr * vsp;
+    }
+
+    DIAG_T(t_phaseA);
+    // ---- multi-hypothesis joint view selection (:994-1056)
     {  // TransformPDFToCDF (:107-121)
         float sum = 0.0f;
         for (int i = 0; i < nsrc; ++i) sum += probs[i];
