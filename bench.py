@@ -7,10 +7,12 @@ Workload (BASELINE.json configs[1], "cfg2"): per GPU, 10 reference views at
 all-gather of the depth maps, then a geometric-consistency pass over the same
 views (it reads the neighbours' depth maps: the real exchange step).
 
-One "step" = photometric pass + all-gather + geometric pass. Views shard one
-contiguous block of 10 per rank on a 10*N-view arc (weak scaling: per-GPU work
-fixed); boundary views read depth maps produced on neighbouring ranks.
-Inputs are rendered straight into HBM before timing (synthetic, seeded).
+One "step" = photometric pass + all-gather + geometric pass. Weak scaling:
+every rank owns one copy of the 10-view cfg2 problem (global view ids
+rank*10 + k), so per-GPU work is identical for every N; the depth maps of all
+ranks are all-gathered (RCCL over xGMI) and the geometric pass reads its
+sources from the gathered buffer. Inputs are rendered straight into HBM before
+timing (synthetic, seeded).
 
 value = total pixels processed by all ranks (2 passes x views x W x H) /
 max-over-ranks wall time of the K timed steps, in Mpix/s.
@@ -55,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="800x600", help="ref-view crop timed on the CPU oracle")
     ap.add_argument("--profile-dir", default=None, help="write per-run timing JSON here")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to test on one GPU)")
     return ap.parse_args()
 
 
@@ -68,22 +72,34 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    backend = args.backend
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from acmmp_amd import ACMMP, default_params, scene
 
+    # Weak scaling: every rank owns one copy of the cfg2 problem (the same
+    # 10-view arc, so per-GPU work is identical for every N); global view id
+    # = rank * views + k. The depth maps of ALL ranks are all-gathered between
+    # the passes and the geometric pass reads its sources from the gathered
+    # buffer, as a view-parallel pipeline does.
+    if args.views < args.nsrc + 1:
+        raise SystemExit(f"--views {args.views} cannot supply {args.nsrc} source views per problem")
     V = args.views * world
     W, H = args.width, args.height
-    setup = scene.scene_setup(num_views=V, width=W, height=H)
-    mine = list(range(rank * args.views, (rank + 1) * args.views))
-    srcs = {v: setup.pairs[v][:args.nsrc] for v in mine}
-    needed = sorted(set(mine) | {s for v in mine for s in srcs[v]})
-    images = {i: scene.render_torch(setup, i, device) for i in needed}
-    cams = {i: setup.camera(i) for i in needed}
+    setup = scene.scene_setup(num_views=args.views, width=W, height=H)
+    base_id = rank * args.views
+    mine = list(range(base_id, base_id + args.views))
+    srcs = {base_id + k: [base_id + j for j in setup.pairs[k][:args.nsrc]] for k in range(args.views)}
+    images = {base_id + k: scene.render_torch(setup, k, device) for k in range(args.views)}
+    cams = {base_id + k: setup.camera(k) for k in range(args.views)}
     torch.cuda.synchronize()
 
     n_img = 1 + args.nsrc
@@ -92,7 +108,7 @@ def main():
     my_depth = torch.empty((args.views, H, W), dtype=torch.float32, device=device)
     all_depth = torch.empty((V, H, W), dtype=torch.float32, device=device) if world > 1 else my_depth
 
-    eng = ACMMP(local_rank)
+    eng = ACMMP(dev_index)
     eng.set_timing(True)
     base = default_params()
     base.max_iterations = args.iters
@@ -108,7 +124,7 @@ def main():
             p.geom_consistency = 1
             p.max_iterations = args.iters  # BASELINE cfg2: 8 iterations in both passes
             eng.set_params(p)
-            # world == 1: all_depth is my_depth and view ids are 0..views-1
+            # global view ids index the gathered maps (world == 1: my_depth)
             eng.set_depth_maps_device([all_depth[i].data_ptr() for i in ids])
             eng.set_plane_hypotheses_device(planes[k].data_ptr(), costs[k].data_ptr())
         eng.run_async()
@@ -120,15 +136,17 @@ def main():
         st[0] += t["sweep_ms"]
         st[1] += t["sweep_launches"]
 
-    if world == 1:
-        # a single GPU must own every source view of the geometric pass
-        assert all(s in mine for v in mine for s in srcs[v])
 
     def step():
         for k, v in enumerate(mine):
             run_view(k, v, geom=False)
         if world > 1:
-            dist.all_gather_into_tensor(all_depth, my_depth)
+            if backend == "nccl":  # RCCL over xGMI, device buffers
+                dist.all_gather_into_tensor(all_depth, my_depth)
+            else:  # gloo (tests on one GPU): staged through host memory
+                host = torch.empty((V, H, W), dtype=torch.float32)
+                dist.all_gather_into_tensor(host, my_depth.cpu())
+                all_depth.copy_(host)
             torch.cuda.synchronize()
         for k, v in enumerate(mine):
             run_view(k, v, geom=True)
@@ -148,7 +166,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -193,7 +211,8 @@ def main():
             "height": H,
             "num_images": n_img,
             "iters": args.iters,
-            "parallelism": f"view-parallel x{world} (one process per GPU, RCCL all-gather of depth maps)",
+            "parallelism": f"view-parallel x{world} (one process per GPU, {'RCCL' if backend == 'nccl' else 'gloo'} "
+                           "all-gather of depth maps between the passes)",
         },
         "roofline": {
             "bound": "hbm",
