@@ -1108,6 +1108,28 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
     // view-major: the 8 candidates of one source view gather from nearly the
     // same footprint, back to back (results are independent)
+#ifdef ACMMP_DIAG_STAMPS
+    {  // duplicate-candidate census: slot 5 = flagged candidates, 6 = equal to an
+       // earlier candidate, 7 = equal to the pixel's current plane
+        unsigned long long n = 0, dup = 0, cur = 0;
+        for (int d = 0; d < 8; ++d) {
+            if (!((flags >> d) & 1u)) continue;
+            const float4 a = cand(d);
+            ++n;
+            bool found = false;
+            for (int e = 0; e < d && !found; ++e)
+                if (((flags >> e) & 1u)) {
+                    const float4 b = cand(e);
+                    found = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+                }
+            dup += found;
+            cur += (a.x == my_plane.x && a.y == my_plane.y && a.z == my_plane.z && a.w == my_plane.w);
+        }
+        atomicAdd(&g_diag_cycles[5], n);
+        atomicAdd(&g_diag_cycles[6], dup);
+        atomicAdd(&g_diag_cycles[7], cur);
+    }
+#endif
     for (int v = 0; v < nsrc; ++v) {
         float cv[8];
 #pragma unroll

@@ -20,3 +20,5 @@ fn(out)
 names = ["tile+search", "pixel_patch", "phaseA_ncc(8 dirs x views)", "view_select+final_costs", "current+refine(6 x sel views)"]
 tot = sum(out[i] for i in range(5))
 print(json.dumps({n: round(out[i] / tot, 4) for i, n in enumerate(names)}))
+print(json.dumps({"candidates": out[5], "dup_of_earlier_candidate": out[6] / max(out[5], 1),
+                  "equal_to_current_plane": out[7] / max(out[5], 1)}))
