@@ -320,15 +320,23 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // normalised ref mean / variance — identical for all 14*(N-1) calls of a
 // pixel-iteration, so computed once (same operations, same order).
 // LDS slot of patch sample (column ii, row jj): in the order the gathers
-// visit them (rows outer with ACMMP_NCC_ROWMAJOR), so consecutive reads are
-// adjacent (ds_read2st64 pairs).
-#ifndef ACMMP_NCC_ROWMAJOR
-#define ACMMP_NCC_ROWMAJOR 1
+// visit them (rows outer), so consecutive reads are adjacent (ds_read2st64).
+DEV int widx(int ii, int jj) { return jj * kTaps + ii; }
+
+// LDS slot per patch sample: (w, w * ref) pairs (ACMMP_LDS_WR=1, 72 KB per
+// block, no per-sample multiply) or w alone (0, 36 KB per block: leaves room
+// for more resident blocks; w * ref is then formed from the ref tile).
+#ifndef ACMMP_LDS_WR
+#define ACMMP_LDS_WR 1
 #endif
-DEV int widx(int ii, int jj) { return ACMMP_NCC_ROWMAJOR ? jj * kTaps + ii : ii * kTaps + jj; }
+#if ACMMP_LDS_WR
+typedef float2 WSlot;
+#else
+typedef float WSlot;
+#endif
 
 struct PixPatch {
-    float2 *w;       // LDS: (w, w * ref) at [k * kThreads] for sample k of this lane
+    WSlot *w;        // LDS: slot of sample k of this lane at [k * kThreads]
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
@@ -364,7 +372,11 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
+#if ACMMP_LDS_WR
             pp.w[widx(ii, jj) * kThreads] = make_float2(w, wr);
+#else
+            pp.w[widx(ii, jj) * kThreads] = w;
+#endif
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -479,8 +491,8 @@ DEV void fetch_row(const SrcImage &im, const float *H, const ColTerms &ct, int p
 }
 
 template <bool FAST>
-DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, int wstride, int px, int py,
-                       float &sum_src, float &sum_ss, float &sum_rs) {
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, int wstride, const float *tile, int tb,
+                       int px, int py, float &sum_src, float &sum_ss, float &sum_rs) {
     ColTerms ct;
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
@@ -507,7 +519,12 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, int
 #pragma unroll
         for (int ii = 0; ii < kTaps; ++ii) {
             const float sv = bilinear_sample(f, ii);
+#if ACMMP_LDS_WR
             const float2 w = wl[widx(ii, jj) * wstride];
+#else
+            const float wv = wl[widx(ii, jj) * wstride];
+            const float2 w = make_float2(wv, wv * tile[tb + ii + 2 * kTileW * jj]);
+#endif
             const float ws = w.x * sv;
             r_s[ii] += ws;
             racc[ii] = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc[ii]);
@@ -525,54 +542,17 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, int
 }
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
-// software-pipelined one patch column ahead (column ii+1's gathers are in
-// flight while column ii is reduced). Returns the three weighted sums.
+// returns the three weighted sums (ncc_sums_rows above).
 template <bool FAST>
 DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb, const PixPatch &pp, int px,
                   int py, float &sum_src, float &sum_ss, float &sum_rs) {
-    sum_src = 0.0f;
-    sum_ss = 0.0f;
-    sum_rs = 0.0f;
     // re-read weights from LDS each call rather than caching them in VGPRs
     // (launder the integer offset, not the pointer, so the LDS address space
     // stays visible and the reads are ds_read, not flat)
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
-    const float2 *wl = pp.w - pp.wo + wo;
-#if ACMMP_NCC_ROWMAJOR
-    ncc_sums_rows<FAST>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
-    return;
-#endif
-#if ACMMP_NCC_PIPELINE
-    ColFetch buf[2];
-    fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
-#endif
-#pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-#if ACMMP_NCC_PIPELINE
-        if (ii + 1 < kTaps) fetch_column<FAST>(im, H, (float)(px - 5 + 2 * (ii + 1)), py, buf[(ii + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const ColFetch &f = buf[ii & 1];
-#else
-        ColFetch f;
-        fetch_column<FAST>(im, H, (float)(px - 5 + 2 * ii), py, f);
-#endif
-        // per column: r_s += ws; (r_ss, r_rs) = fma((ws, wr), sv, (r_ss, r_rs))
-        float r_s = 0.0f;
-        f2v racc = f2v{0.0f, 0.0f};
-#pragma unroll
-        for (int jj = 0; jj < kTaps; ++jj) {
-            const float sv = bilinear_sample(f, jj);
-            const float2 w = wl[widx(ii, jj) * kThreads];
-            const float ws = w.x * sv;
-            r_s += ws;
-            racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
-        }
-        sum_src += r_s;
-        sum_ss += racc.x;
-        sum_rs += racc.y;
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    const WSlot *wl = pp.w - pp.wo + wo;
+    ncc_sums_rows<FAST>(im, H, wl, kThreads, tile, tb, px, py, sum_src, sum_ss, sum_rs);
 }
 
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
@@ -824,7 +804,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 template <int NS>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSamples * kThreads];
+    __shared__ WSlot wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -915,7 +895,7 @@ template <int NS>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSamples * kThreads];
+    __shared__ WSlot wlds[kSamples * kThreads];
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -1452,7 +1432,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSamples * kThreads];
+    __shared__ WSlot wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1580,14 +1560,14 @@ __global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int 
     out[(size_t)py * W + px] = total_val / normalizing_factor;
 }
 
-#ifdef ACMMP_DIAG_PROBE
+#if defined(ACMMP_DIAG_PROBE) && ACMMP_LDS_WR
 // ---- throughput probe (diagnostic builds only): one thread per (pixel,
 // candidate), the pixel's 36 (w, w*r) pairs precomputed and staged in LDS,
 // NCC against every source view; measures the split-kernel design.
 __global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ kvp, int colour, float2 *wpair,
                                                     float4 *stats, int P2) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSamples * kThreads];
+    __shared__ WSlot wlds[kSamples * kThreads];
     const KViews &kv = *kvp;
     const BlockXY blk{(int)blockIdx.x, (int)blockIdx.y};
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
@@ -1668,7 +1648,8 @@ __global__ __launch_bounds__(576) void k_probe(const KViews *__restrict__ kvp, K
             const float2 pt = project(H, (float)px, (float)py);
             if (!(pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f)) {
                 float sum_src, sum_ss, sum_rs;
-                if (PIPE == 2) ncc_sums_rows<true>(im, H, &wl[0][lane], 64, px, py, sum_src, sum_ss, sum_rs);
+                if (PIPE == 2)
+                    ncc_sums_rows<true>(im, H, &wl[0][lane], 64, nullptr, 0, px, py, sum_src, sum_ss, sum_rs);
                 else ncc_sums_lean<true, PIPE>(im, H, wl, lane, px, py, sum_src, sum_ss, sum_rs);
                 sum_src *= ps.z;
                 sum_ss *= ps.z;
