@@ -196,6 +196,9 @@ SIGNATURES = {
                                         C.POINTER(PassOptions)]),
     "acmmp_joint_bilateral_upsampling": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int]),
     "acmmp_pipeline_last_error": (C.c_char_p, []),
+    "acmmp_run_fusion": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int, C.c_float, C.c_int,
+                                   C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)]),
+    "acmmp_fusion_last_error": (C.c_char_p, []),
     "acmmp_priors_available": (C.c_int, [C.c_char_p, C.c_int]),
     "acmmp_prior_plane_estimate": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(Camera), C.c_int, C.c_int, _FP]),
     "acmmp_read_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint16), C.c_size_t, C.POINTER(C.c_int),
@@ -203,6 +206,8 @@ SIGNATURES = {
     "acmmp_get_reference_image": (C.c_int, [_CTX, _FP, C.c_size_t]),
     "acmmp_prior_plane_params": (C.c_int, [C.POINTER(Camera), _I32P, _FP, _FP]),
     "acmmp_depth_from_plane_param": (C.c_float, [C.POINTER(Camera), _FP, C.c_int, C.c_int]),
+    "acmmp_read_image_bgr": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_int),
+                                       C.POINTER(C.c_int)]),
     "acmmp_read_image_gray": (C.c_int, [C.c_char_p, _FP, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_image_size": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_resize_linear": (C.c_int, [_FP, C.c_int, C.c_int, _FP, C.c_int, C.c_int]),

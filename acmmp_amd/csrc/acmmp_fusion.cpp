@@ -1,0 +1,318 @@
+// acmmp_fusion.cpp — RunFusion (src/acmmp_definitions.cpp:828-1043), SURVEY
+// §8f rank 3: depth/normal maps of all views -> one coloured point cloud
+// (<out>/ACMMP_model.ply, StoreColorPlyFileBinaryPointCloud src/ACMMP.cpp:
+// 382-424).
+//
+// Host code, literal: the reference's fusion is order-dependent (a pixel's
+// approval masks pixels of other views that later pixels then skip, and
+// used_list is never reset between pixels), so it runs sequentially in the
+// reference's order with the reference's float expression order
+// (Get3DPointonWorld / ProjectonCamera src/ACMMP.cpp:203-251, GetAngle
+// :253-262). Deviations: no cv::imshow (:897-900); the PLY is written in
+// point order (the reference's OpenMP-critical writes make its order
+// arbitrary); a colour image whose size differs from its depth map is resized
+// with a float bilinear filter (cv::resize's 8-bit fixed-point path is
+// unpinned).
+#include <sys/stat.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/acmmp.h"
+
+namespace {
+
+thread_local std::string f_err;
+
+int ffail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    f_err = buf;
+    return code;
+}
+
+std::string id8(int id) {
+    char b[32];
+    std::snprintf(b, sizeof(b), "%08d", id);
+    return b;
+}
+
+struct F3 {
+    float x, y, z;
+};
+
+F3 world_point(int x, int y, float depth, const acmmp_camera &c) {  // Get3DPointonWorld
+    F3 p;
+    p.x = depth * (x - c.K[2]) / c.K[0];
+    p.y = depth * (y - c.K[5]) / c.K[4];
+    p.z = depth;
+    F3 t;
+    t.x = c.R[0] * p.x + c.R[3] * p.y + c.R[6] * p.z;
+    t.y = c.R[1] * p.x + c.R[4] * p.y + c.R[7] * p.z;
+    t.z = c.R[2] * p.x + c.R[5] * p.y + c.R[8] * p.z;
+    F3 C;
+    C.x = -(c.R[0] * c.t[0] + c.R[3] * c.t[1] + c.R[6] * c.t[2]);
+    C.y = -(c.R[1] * c.t[0] + c.R[4] * c.t[1] + c.R[7] * c.t[2]);
+    C.z = -(c.R[2] * c.t[0] + c.R[5] * c.t[1] + c.R[8] * c.t[2]);
+    p.x = t.x + C.x;
+    p.y = t.y + C.y;
+    p.z = t.z + C.z;
+    return p;
+}
+
+void project(const F3 &X, const acmmp_camera &c, float &px, float &py, float &depth) {  // ProjectonCamera
+    F3 t;
+    t.x = c.R[0] * X.x + c.R[1] * X.y + c.R[2] * X.z + c.t[0];
+    t.y = c.R[3] * X.x + c.R[4] * X.y + c.R[5] * X.z + c.t[1];
+    t.z = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
+    depth = c.K[6] * t.x + c.K[7] * t.y + c.K[8] * t.z;
+    px = (c.K[0] * t.x + c.K[1] * t.y + c.K[2] * t.z) / depth;
+    py = (c.K[3] * t.x + c.K[4] * t.y + c.K[5] * t.z) / depth;
+}
+
+float get_angle(const float *a, const float *b) {  // GetAngle
+    const float dot = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+    const float angle = std::acos(dot);
+    if (angle != angle) return 0.0f;
+    return angle;
+}
+
+int read_dmb(const std::string &path, std::vector<float> &d, int &h, int &w, int &nb) {
+    int32_t hh = 0, ww = 0, bb = 0;
+    int rc = acmmp_read_dmb(path.c_str(), &hh, &ww, &bb, nullptr, 0);
+    if (rc != ACMMP_OK && rc != ACMMP_ERR_ARG) return ffail(ACMMP_ERR_IO, "cannot read %s", path.c_str());
+    d.resize((size_t)hh * ww * bb);
+    if (acmmp_read_dmb(path.c_str(), &hh, &ww, &bb, d.data(), d.size()))
+        return ffail(ACMMP_ERR_IO, "cannot read %s", path.c_str());
+    h = hh;
+    w = ww;
+    nb = bb;
+    return ACMMP_OK;
+}
+
+// Float bilinear resize of an 8-bit multi-channel image (half-pixel centres,
+// edge clamp, round to nearest) — the unpinned stand-in for cv::resize.
+void resize_u8(const std::vector<uint8_t> &src, int sw, int sh, int C, std::vector<uint8_t> &dst, int dw, int dh) {
+    dst.resize((size_t)dw * dh * C);
+    for (int y = 0; y < dh; ++y) {
+        float fy = (float)((y + 0.5) * sh / dh - 0.5);
+        int y0 = (int)std::floor(fy);
+        float ay = fy - y0;
+        if (y0 < 0) { y0 = 0; ay = 0; }
+        if (y0 >= sh - 1) { y0 = sh - 1; ay = 0; }
+        const int y1 = std::min(y0 + 1, sh - 1);
+        for (int x = 0; x < dw; ++x) {
+            float fx = (float)((x + 0.5) * sw / dw - 0.5);
+            int x0 = (int)std::floor(fx);
+            float ax = fx - x0;
+            if (x0 < 0) { x0 = 0; ax = 0; }
+            if (x0 >= sw - 1) { x0 = sw - 1; ax = 0; }
+            const int x1 = std::min(x0 + 1, sw - 1);
+            for (int k = 0; k < C; ++k) {
+                auto at = [&](int yy, int xx) { return (float)src[((size_t)yy * sw + xx) * C + k]; };
+                const float top = at(y0, x0) * (1 - ax) + at(y0, x1) * ax;
+                const float bot = at(y1, x0) * (1 - ax) + at(y1, x1) * ax;
+                const float v = top * (1 - ay) + bot * ay;
+                dst[((size_t)y * dw + x) * C + k] = (uint8_t)std::min(255.0f, std::max(0.0f, std::nearbyint(v)));
+            }
+        }
+    }
+}
+
+struct Point {
+    F3 coord, normal, color;
+};
+
+int store_ply(const std::string &path, const std::vector<Point> &pc) {  // StoreColorPlyFileBinaryPointCloud
+    FILE *f = std::fopen(path.c_str(), "wb");
+    if (!f) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    std::fprintf(f, "ply\nformat binary_little_endian 1.0\nelement vertex %d\n", (int)pc.size());
+    std::fprintf(f, "property float x\nproperty float y\nproperty float z\n");
+    std::fprintf(f, "property float nx\nproperty float ny\nproperty float nz\n");
+    std::fprintf(f, "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n");
+    for (const Point &p : pc) {
+        F3 X = p.coord;
+        const char b = (char)(int)p.color.x, g = (char)(int)p.color.y, r = (char)(int)p.color.z;
+        if (!(X.x < FLT_MAX && X.x > -FLT_MAX) || !(X.y < FLT_MAX && X.y > -FLT_MAX) ||
+            !(X.z < FLT_MAX && X.z >= -FLT_MAX)) {
+            X.x = X.y = X.z = 0.0f;
+        }
+        const float v[6] = {X.x, X.y, X.z, p.normal.x, p.normal.y, p.normal.z};
+        std::fwrite(v, sizeof(float), 6, f);
+        std::fwrite(&r, 1, 1, f);
+        std::fwrite(&g, 1, 1, f);
+        std::fwrite(&b, 1, 1, f);
+    }
+    std::fclose(f);
+    return ACMMP_OK;
+}
+
+}  // namespace
+
+// in acmmp_pipeline.cpp (zlib PNG writer)
+int acmmp_internal_write_png_gray(const char *path, int w, int h, const uint8_t *px);
+
+extern "C" {
+
+const char *acmmp_fusion_last_error(void) { return f_err.c_str(); }
+
+int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const acmmp_problem *problems, int count,
+                     int geom_consistency, float consistency_scalar, int con_num_thresh, const char *image_dir,
+                     const char *mask_folder, int write_debug_images, int *num_points) {
+    if (!dense_folder || !output_folder || !problems || count <= 0) return ffail(ACMMP_ERR_ARG, "bad args");
+    const std::string dense = dense_folder, out = output_folder;
+    const std::string image_folder = dense + (image_dir ? image_dir : "/images");
+    const std::string cam_folder = dense + "/cams";
+    const bool use_masks = mask_folder && std::string(mask_folder) != " " && mask_folder[0] != 0;
+    const size_t n = (size_t)count;
+    std::vector<std::vector<uint8_t>> images(n), masks(n);
+    std::vector<acmmp_camera> cameras(n);
+    std::vector<std::vector<float>> depths(n), normals(n);
+    std::vector<int> rows(n), cols(n);
+    std::map<int, int> image_id_2_index;
+    for (size_t i = 0; i < n; ++i) {
+        const int id = problems[i].ref_image_id;
+        image_id_2_index[id] = (int)i;
+        const std::string ipath = image_folder + "/" + id8(id) + ".jpg";
+        int iw = 0, ih = 0;
+        std::vector<uint8_t> img;
+        int rc = acmmp_read_image_bgr(ipath.c_str(), nullptr, 0, &iw, &ih);
+        if (rc == ACMMP_ERR_ARG) {
+            img.resize((size_t)iw * ih * 3);
+            rc = acmmp_read_image_bgr(ipath.c_str(), img.data(), img.size(), &iw, &ih);
+        }
+        if (rc) return ffail(rc, "cannot read image %s", ipath.c_str());
+        const std::string cpath = cam_folder + "/" + id8(id) + "_cam.txt";
+        if (acmmp_read_camera(cpath.c_str(), &cameras[i])) return ffail(ACMMP_ERR_IO, "cannot read %s", cpath.c_str());
+        const std::string rf = out + "/2333_" + id8(id);
+        int h, w, nb, h2, w2, nb2;
+        rc = read_dmb(rf + (geom_consistency ? "/depths_geom.dmb" : "/depths.dmb"), depths[i], h, w, nb);
+        if (!rc) rc = read_dmb(rf + "/normals.dmb", normals[i], h2, w2, nb2);
+        if (rc) return rc;
+        if (nb != 1 || nb2 != 3 || h2 != h || w2 != w) return ffail(ACMMP_ERR_IO, "bad maps for view %d", id);
+        rows[i] = h;
+        cols[i] = w;
+        // RescaleImageAndCamera (src/ACMMP.cpp:181-201)
+        if (w == iw && h == ih) {
+            images[i] = std::move(img);
+        } else {
+            const float scale_x = w / static_cast<float>(iw);
+            const float scale_y = h / static_cast<float>(ih);
+            resize_u8(img, iw, ih, 3, images[i], w, h);
+            cameras[i].K[0] *= scale_x;
+            cameras[i].K[2] *= scale_x;
+            cameras[i].K[4] *= scale_y;
+            cameras[i].K[5] *= scale_y;
+            cameras[i].width = w;
+            cameras[i].height = h;
+        }
+        masks[i].assign((size_t)w * h, 0);
+        if (use_masks) {  // :881-905: mask = (resize(mask) < 128) / 255
+            const std::string mpath = dense + "/" + mask_folder + "/" + id8(id) + ".png";
+            int mw = 0, mh = 0, mc = 0, bd = 0;
+            std::vector<uint16_t> m16;
+            rc = acmmp_read_png(mpath.c_str(), nullptr, 0, &mw, &mh, &mc, &bd);
+            if (rc == ACMMP_ERR_ARG) {
+                m16.resize((size_t)mw * mh * mc);
+                rc = acmmp_read_png(mpath.c_str(), m16.data(), m16.size(), &mw, &mh, &mc, &bd);
+            }
+            if (rc || bd != 8) return ffail(ACMMP_ERR_IO, "Couldn't find mask image %s", mpath.c_str());
+            std::vector<uint8_t> m8((size_t)mw * mh), mr;
+            for (size_t k = 0; k < m8.size(); ++k) m8[k] = (uint8_t)m16[k * mc];
+            resize_u8(m8, mw, mh, 1, mr, w, h);
+            for (size_t k = 0; k < mr.size(); ++k) masks[i][k] = mr[k] < 128 ? 1 : 0;
+        }
+    }
+
+    std::vector<Point> cloud;
+    for (size_t i = 0; i < n; ++i) {
+        const int W = cols[i], H = rows[i];
+        const int num_ngb = problems[i].num_src_images;
+        const float depth_max = cameras[i].depth_max;
+        std::vector<int> used_x(num_ngb, -1), used_y(num_ngb, -1);
+        std::vector<uint8_t> approved((size_t)W * H, 0);
+        std::vector<int> src_index(num_ngb);
+        for (int j = 0; j < num_ngb; ++j) {
+            auto it = image_id_2_index.find(problems[i].src_image_ids[j]);
+            if (it == image_id_2_index.end())
+                return ffail(ACMMP_ERR_ARG, "source %d of view %d is not a problem", problems[i].src_image_ids[j],
+                             problems[i].ref_image_id);
+            src_index[j] = it->second;
+        }
+        for (int r = 0; r < H; ++r) {
+            for (int c = 0; c < W; ++c) {
+                const size_t pc = (size_t)r * W + c;
+                if (masks[i][pc] == 1) continue;
+                const float ref_depth = depths[i][pc];
+                const float *ref_normal = &normals[i][pc * 3];
+                if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
+                const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
+                const uint8_t *bgr = &images[i][pc * 3];
+                int num_consistent = 0;
+                float dynamic_consistency = 0;
+                for (int j = 0; j < num_ngb; ++j) {
+                    const int s = src_index[j];
+                    const int src_cols = cols[s], src_rows = rows[s];
+                    float ptx, pty, proj_depth;
+                    project(PointX, cameras[s], ptx, pty, proj_depth);
+                    const int src_r = int(pty + 0.5f);
+                    const int src_c = int(ptx + 0.5f);
+                    if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
+                        const size_t sp = (size_t)src_r * src_cols + src_c;
+                        if (masks[s][sp] == 1) continue;
+                        const float src_depth = depths[s][sp];
+                        const float *src_normal = &normals[s][sp * 3];
+                        if (src_depth <= 0.0) continue;
+                        const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
+                        float tx, ty;
+                        project(tmp_X, cameras[i], tx, ty, proj_depth);
+                        const float reproj_error = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
+                        const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
+                        const float angle = get_angle(ref_normal, src_normal);
+                        if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
+                            used_x[j] = src_c;
+                            used_y[j] = src_r;
+                            const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
+                            dynamic_consistency += std::exp(-tmp_index);
+                            num_consistent++;
+                        }
+                    }
+                }
+                if (num_consistent >= con_num_thresh &&
+                    (dynamic_consistency > consistency_scalar * num_consistent)) {
+                    Point p;
+                    p.coord = PointX;
+                    p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
+                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
+                    cloud.push_back(p);
+                    // used_list is not reset per pixel in the reference: stale entries apply too
+                    for (int j = 0; j < num_ngb; ++j) {
+                        if (used_x[j] == -1) continue;
+                        const int s = src_index[j];
+                        masks[s][(size_t)used_y[j] * cols[s] + used_x[j]] = 1;
+                        // `approved` is this view's W x H image indexed by source coordinates (:1030)
+                        if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
+                    }
+                }
+            }
+        }
+        if (write_debug_images) {
+            const std::string dbg = dense + "/approved_pixels_cam_" + std::to_string(i) + ".png";
+            if (acmmp_internal_write_png_gray(dbg.c_str(), W, H, approved.data()))
+                return ffail(ACMMP_ERR_IO, "cannot write %s", dbg.c_str());
+        }
+    }
+    if (num_points) *num_points = (int)cloud.size();
+    return store_ply(out + "/ACMMP_model.ply", cloud);
+}
+
+}  // extern "C"

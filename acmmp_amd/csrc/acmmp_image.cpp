@@ -234,7 +234,7 @@ bool decode_scan(Jpeg &j, const uint8_t *hdr, int len) {
                         const int gx = ns == 1 ? mx : mx * c.h + bx;
                         const int gy = ns == 1 ? my : my * c.v + by;
                         int16_t *dst = nullptr;
-                        if (sc[i] == 0 && gx < c.bw && gy < c.bh) dst = &c.coef[((size_t)gy * c.bw + gx) * 64];
+                        if (!c.coef.empty() && gx < c.bw && gy < c.bh) dst = &c.coef[((size_t)gy * c.bw + gx) * 64];
                         decode_block(j, c, dst);
                         if (j.err) return false;
                     }
@@ -359,9 +359,86 @@ void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) 
     }
 }
 
+// ---- colour output (cv::imread IMREAD_COLOR = libjpeg JCS_RGB, reordered to
+// BGR): chroma planes upsampled with libjpeg's default "fancy" triangle
+// filters (jdsample.c h2v1 / h2v2; other ratios replicate), then the
+// fixed-point YCbCr->RGB of jdcolor.c (16-bit tables, range-limited).
+void h2v1_fancy(const uint8_t *in, int dw, uint8_t *out) {
+    if (dw < 2) {
+        out[0] = out[1] = in[0];
+        return;
+    }
+    out[0] = in[0];
+    out[1] = (uint8_t)((in[0] * 3 + in[1] + 2) >> 2);
+    for (int c = 1; c < dw - 1; ++c) {
+        const int v = in[c] * 3;
+        out[2 * c] = (uint8_t)((v + in[c - 1] + 1) >> 2);
+        out[2 * c + 1] = (uint8_t)((v + in[c + 1] + 2) >> 2);
+    }
+    const int c = dw - 1;
+    out[2 * c] = (uint8_t)((in[c] * 3 + in[c - 1] + 1) >> 2);
+    out[2 * c + 1] = in[c];
+}
+
+void h2v2_fancy_row(const uint8_t *in0, const uint8_t *in1, int dw, uint8_t *out) {
+    if (dw < 2) {
+        out[0] = out[1] = (uint8_t)(((in0[0] * 3 + in1[0]) * 4 + 8) >> 4);
+        return;
+    }
+    int thiscolsum = in0[0] * 3 + in1[0];
+    int nextcolsum = in0[1] * 3 + in1[1];
+    out[0] = (uint8_t)((thiscolsum * 4 + 8) >> 4);
+    out[1] = (uint8_t)((thiscolsum * 3 + nextcolsum + 7) >> 4);
+    int lastcolsum = thiscolsum;
+    thiscolsum = nextcolsum;
+    for (int c = 1; c < dw - 1; ++c) {
+        nextcolsum = in0[c + 1] * 3 + in1[c + 1];
+        out[2 * c] = (uint8_t)((thiscolsum * 3 + lastcolsum + 8) >> 4);
+        out[2 * c + 1] = (uint8_t)((thiscolsum * 3 + nextcolsum + 7) >> 4);
+        lastcolsum = thiscolsum;
+        thiscolsum = nextcolsum;
+    }
+    const int c = dw - 1;
+    out[2 * c] = (uint8_t)((thiscolsum * 3 + lastcolsum + 8) >> 4);
+    out[2 * c + 1] = (uint8_t)((thiscolsum * 4 + 7) >> 4);
+}
+
+// Component plane at full resolution (W x H): IDCT, then upsampling.
+void component_full(const Comp &c, const uint16_t *q, int W, int H, int hmax, int vmax, std::vector<uint8_t> &out) {
+    const int pw = c.bw * 8, ph = c.bh * 8;
+    std::vector<uint8_t> plane((size_t)pw * ph);
+    for (int by = 0; by < c.bh; ++by)
+        for (int bx = 0; bx < c.bw; ++bx)
+            idct_islow(&c.coef[((size_t)by * c.bw + bx) * 64], q, &plane[(size_t)by * 8 * pw + bx * 8], pw);
+    const int dw = (int)(((long)W * c.h + hmax - 1) / hmax), dh = (int)(((long)H * c.v + vmax - 1) / vmax);
+    const int fx = hmax / c.h, fy = vmax / c.v;
+    out.assign((size_t)W * H, 0);
+    std::vector<uint8_t> row((size_t)2 * dw + 2);
+    for (int y = 0; y < H; ++y) {
+        uint8_t *o = &out[(size_t)y * W];
+        if (fx == 1 && fy == 1) {
+            std::memcpy(o, &plane[(size_t)y * pw], W);
+        } else if (fx == 2 && fy == 1) {
+            h2v1_fancy(&plane[(size_t)y * pw], dw, row.data());
+            std::memcpy(o, row.data(), W);
+        } else if (fx == 2 && fy == 2) {
+            const int r = y >> 1;
+            const int nr = (y & 1) ? std::min(r + 1, dh - 1) : std::max(r - 1, 0);  // context rows replicate edges
+            h2v2_fancy_row(&plane[(size_t)r * pw], &plane[(size_t)nr * pw], dw, row.data());
+            std::memcpy(o, row.data(), W);
+        } else {
+            const uint8_t *src = &plane[(size_t)(y / fy) * pw];
+            for (int x = 0; x < W; ++x) o[x] = src[x / fx];
+        }
+    }
+}
+
+inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
 // Parses markers up to the first SOS (size_only) or decodes the luminance
-// plane into `gray` (W*H bytes).
-int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H, std::vector<uint8_t> *gray) {
+// plane into `gray` (W*H bytes), or with `bgr` the colour image (W*H*3, BGR).
+int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H, std::vector<uint8_t> *gray,
+                std::vector<uint8_t> *bgr = nullptr) {
     Jpeg j;
     j.p = buf.data();
     j.end = buf.data() + buf.size();
@@ -415,6 +492,16 @@ int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H,
             y.bw = mcus_x * y.h;
             y.bh = mcus_y * y.v;
             y.coef.assign((size_t)y.bw * y.bh * 64, 0);
+            if (bgr) {
+                if (j.ncomp != 1 && j.ncomp != 3) return ACMMP_ERR_UNSUPPORTED;  // CMYK / YCCK
+                for (int c = 1; c < j.ncomp; ++c) {
+                    Comp &cp = j.comp[c];
+                    if (j.hmax % cp.h || j.vmax % cp.v) return ACMMP_ERR_UNSUPPORTED;
+                    cp.bw = mcus_x * cp.h;
+                    cp.bh = mcus_y * cp.v;
+                    cp.coef.assign((size_t)cp.bw * cp.bh * 64, 0);
+                }
+            }
         } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
             return ACMMP_ERR_UNSUPPORTED;  // progressive, lossless, arithmetic
         } else if (m == 0xDB) {  // DQT
@@ -451,6 +538,38 @@ int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H,
     if (!j.sof) return ACMMP_ERR_IO;
     if (size_only) return ACMMP_OK;
     if (!decoded || !j.qt_present[j.comp[0].tq]) return ACMMP_ERR_IO;
+    if (bgr) {
+        std::vector<uint8_t> planes[3];
+        for (int c = 0; c < j.ncomp; ++c) {
+            if (!j.qt_present[j.comp[c].tq]) return ACMMP_ERR_IO;
+            component_full(j.comp[c], j.qt[j.comp[c].tq], j.W, j.H, j.hmax, j.vmax, planes[c]);
+        }
+        const size_t P = (size_t)j.W * j.H;
+        bgr->resize(P * 3);
+        if (j.ncomp == 1) {
+            for (size_t i = 0; i < P; ++i) (*bgr)[3 * i] = (*bgr)[3 * i + 1] = (*bgr)[3 * i + 2] = planes[0][i];
+            return ACMMP_OK;
+        }
+        // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert
+        const int SB = 16;
+        const long ONE_HALF = 1L << (SB - 1);
+        auto FIX = [](double x) { return (long)(x * (1L << 16) + 0.5); };
+        int cr_r[256], cb_b[256];
+        long cr_g[256], cb_g[256];
+        for (int i = 0, x = -128; i < 256; ++i, ++x) {
+            cr_r[i] = (int)((FIX(1.40200) * x + ONE_HALF) >> SB);
+            cb_b[i] = (int)((FIX(1.77200) * x + ONE_HALF) >> SB);
+            cr_g[i] = (-FIX(0.71414)) * x;
+            cb_g[i] = (-FIX(0.34414)) * x + ONE_HALF;
+        }
+        for (size_t i = 0; i < P; ++i) {
+            const int yv = planes[0][i], cb = planes[1][i], cr = planes[2][i];
+            (*bgr)[3 * i + 2] = clamp255(yv + cr_r[cr]);
+            (*bgr)[3 * i + 1] = clamp255(yv + (int)((cb_g[cb] + cr_g[cr]) >> SB));
+            (*bgr)[3 * i + 0] = clamp255(yv + cb_b[cb]);
+        }
+        return ACMMP_OK;
+    }
     const Comp &y = j.comp[0];
     const int pw = y.bw * 8, ph = y.bh * 8;
     std::vector<uint8_t> full((size_t)pw * ph);
@@ -688,6 +807,34 @@ int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *wi
     *height = H;
     if (!out || capacity < img.size()) return ACMMP_ERR_ARG;
     std::memcpy(out, img.data(), img.size() * sizeof(float));
+    return ACMMP_OK;
+}
+
+int acmmp_read_image_bgr(const char *path, uint8_t *out, size_t capacity, int *width, int *height) {
+    if (!width || !height) return ACMMP_ERR_ARG;
+    std::vector<uint8_t> buf;
+    if (!path || !read_file(path, buf)) return ACMMP_ERR_IO;
+    int W = 0, H = 0;
+    std::vector<uint8_t> bgr;
+    int rc;
+    if (buf.size() >= 2 && buf[0] == 0xFF && buf[1] == 0xD8) {
+        rc = jpeg_decode(buf, false, W, H, nullptr, &bgr);
+    } else {
+        int C = 0, depth = 0;
+        std::vector<uint16_t> px;
+        rc = png_decode(buf, W, H, C, depth, &px);
+        if (!rc) {
+            if (depth != 8) return ACMMP_ERR_UNSUPPORTED;
+            bgr.resize((size_t)W * H * 3);
+            for (size_t i = 0; i < (size_t)W * H; ++i)
+                for (int k = 0; k < 3; ++k) bgr[3 * i + k] = (uint8_t)px[i * C + (C >= 3 ? k : 0)];
+        }
+    }
+    if (rc) return rc;
+    *width = W;
+    *height = H;
+    if (!out || capacity < bgr.size()) return ACMMP_ERR_ARG;
+    std::memcpy(out, bgr.data(), bgr.size());
     return ACMMP_OK;
 }
 

@@ -4,9 +4,10 @@
 // hierarchy pass on finer scales. Views are processed in order within a pass
 // (the reference's Gauss-Seidel schedule). No GUI calls.
 //
-// Fusion (RunFusion / RunPriorAwareFusion) is not part of this build; the
-// fusion options are accepted so existing command lines keep working, and the
-// .dmb outputs are the reference's, for its fuse_data.
+// After the passes it fuses the maps like main_ACMMP (:178-199) with the
+// library's RunFusion port (acmmp_fusion.cpp) into <out>/ACMMP_model.ply;
+// RunPriorAwareFusion (--multi_fusion with -p, or --force_fusion) is not
+// ported: the maps are written and the reference's fuse_data can be used.
 #include <sys/stat.h>
 
 #include <cmath>
@@ -30,8 +31,12 @@ void usage() {
         "  --seed N                 base RNG seed (default 1234)\n"
         "  --no_triangulation       do not write triangulation.png\n"
         "  --quiet                  no progress output\n"
-        "  fusion options accepted and ignored: -f/--fuse_thresh, --multi_fusion, --force_fusion,\n"
-        "  --num_consistent_thresh, --single_match_penalty, --mask_dir, --image_override\n");
+        "  -f, --fuse_thresh X      average inverse score threshold for fusion (0.3)\n"
+        "  --num_consistent_thresh N  consistent views needed to fuse a point (1)\n"
+        "  --mask_dir DIR           boolean masks (0, 255) under <dense>/DIR\n"
+        "  --image_override DIR     texture images for fusion (default /images)\n"
+        "  --no_fusion              stop after the depth/normal/cost maps\n"
+        "  --multi_fusion / --force_fusion / --single_match_penalty: prior-aware fusion (not ported)\n");
 }
 
 int die(const char *what) {
@@ -42,8 +47,11 @@ int die(const char *what) {
 }  // namespace
 
 int main(int argc, char **argv) {
-    std::string dense_folder, output_dir = "/ACMMP";
-    bool prior = false, quiet = false, triangulation = true, renamed_outdir = false;
+    std::string dense_folder, output_dir = "/ACMMP", mask_dir = " ", image_dir = "/images";
+    bool prior = false, quiet = false, triangulation = true, renamed_outdir = false, fusion = true;
+    bool multi_fusion = false, force_fusion = false;
+    float consistency_scalar = 0.3f;
+    int num_consistent_thresh = 1;
     int device = 0, iterations = 0;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
@@ -73,12 +81,23 @@ int main(int argc, char **argv) {
             triangulation = false;
         } else if (a == "--quiet") {
             quiet = true;
-        } else if (a == "-f" || a == "--fuse_thresh" || a == "--num_consistent_thresh" ||
-                   a == "--single_match_penalty" || a == "--mask_dir" || a == "--image_override") {
+        } else if (a == "-f" || a == "--fuse_thresh") {
+            consistency_scalar = (float)std::atof(value().c_str());
+        } else if (a == "--num_consistent_thresh") {
+            num_consistent_thresh = std::atoi(value().c_str());
+        } else if (a == "--mask_dir") {
+            mask_dir = value();
+        } else if (a == "--image_override") {
+            image_dir = value();
+        } else if (a == "--single_match_penalty") {
             value();
+        } else if (a == "--no_fusion") {
+            fusion = false;
         } else if (a == "--multi_fusion") {
+            multi_fusion = true;
             if (i + 1 < argc && argv[i + 1][0] != '-') ++i;
         } else if (a == "--force_fusion") {
+            force_fusion = true;
         } else if (!a.empty() && a[0] != '-' && dense_folder.empty()) {
             dense_folder = a;
         } else {
@@ -159,7 +178,18 @@ int main(int argc, char **argv) {
             if (!run_pass(true, false, false, g > 0)) return die("ProcessProblem");
         max_num_downscale--;
     }
-    if (!quiet) std::printf("Depth/normal/cost maps written under %s (fusion not run by this build)\n",
-                            output_folder.c_str());
+    if (!fusion) return 0;
+    if ((prior && multi_fusion) || force_fusion) {
+        std::printf("Prior-aware fusion is not ported; maps are under %s for the reference's fuse_data\n",
+                    output_folder.c_str());
+        return 0;
+    }
+    int npts = 0;
+    if (acmmp_run_fusion(dense_folder.c_str(), output_folder.c_str(), problems.data(), num_images, 1,
+                         consistency_scalar, num_consistent_thresh, image_dir.c_str(), mask_dir.c_str(), 1, &npts)) {
+        std::fprintf(stderr, "acmmp_main: RunFusion: %s\n", acmmp_fusion_last_error());
+        return 1;
+    }
+    if (!quiet) std::printf("Fused %d points into %s/ACMMP_model.ply\n", npts, output_folder.c_str());
     return 0;
 }

@@ -104,12 +104,12 @@ void put_chunk(std::vector<uint8_t> &png, const char *type, const std::vector<ui
     png.insert(png.end(), c, c + 4);
 }
 
-int write_png_rgb(const std::string &path, int w, int h, const std::vector<uint8_t> &rgb) {
+int write_png8(const std::string &path, int w, int h, int channels, const uint8_t *px) {
     std::vector<uint8_t> raw;
-    raw.reserve((size_t)h * (3 * w + 1));
+    raw.reserve((size_t)h * (channels * w + 1));
     for (int y = 0; y < h; ++y) {
         raw.push_back(0);
-        raw.insert(raw.end(), rgb.begin() + (size_t)y * 3 * w, rgb.begin() + (size_t)(y + 1) * 3 * w);
+        raw.insert(raw.end(), px + (size_t)y * channels * w, px + (size_t)(y + 1) * channels * w);
     }
     uLongf zlen = compressBound((uLong)raw.size());
     std::vector<uint8_t> z(zlen);
@@ -119,7 +119,7 @@ int write_png_rgb(const std::string &path, int w, int h, const std::vector<uint8
     std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     std::vector<uint8_t> ihdr = {(uint8_t)(w >> 24), (uint8_t)(w >> 16), (uint8_t)(w >> 8), (uint8_t)w,
                                  (uint8_t)(h >> 24), (uint8_t)(h >> 16), (uint8_t)(h >> 8), (uint8_t)h,
-                                 8, 2, 0, 0, 0};
+                                 8, (uint8_t)(channels == 3 ? 2 : 0), 0, 0, 0};
     put_chunk(png, "IHDR", ihdr);
     put_chunk(png, "IDAT", z);
     put_chunk(png, "IEND", {});
@@ -171,7 +171,7 @@ int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
         draw_line(rgb, W, H, t.pt1, t.pt3);
         draw_line(rgb, W, H, t.pt2, t.pt3);
     }
-    return write_png_rgb(path, W, H, rgb);
+    return write_png8(path, W, H, 3, rgb.data());
 }
 
 // One view of InputInitialization (src/ACMMP.cpp:536-598): image + camera,
@@ -248,6 +248,11 @@ void depth_normal_to_plane(float depth, float nx, float ny, float nz, int px, in
 }
 
 }  // namespace
+
+// 8-bit grayscale PNG for the fusion's debug images (acmmp_fusion.cpp)
+int acmmp_internal_write_png_gray(const char *path, int w, int h, const uint8_t *px) {
+    return write_png8(path, w, h, 1, px);
+}
 
 extern "C" {
 

@@ -166,3 +166,19 @@ def resize_linear(img: np.ndarray, width: int, height: int) -> np.ndarray:
     if rc != 0:
         raise ValueError(f"acmmp_resize_linear failed (status {rc})")
     return out
+
+
+def read_image_bgr(path: str) -> np.ndarray:
+    """cv::imread(path, IMREAD_COLOR) -> (H, W, 3) uint8 BGR (baseline JPEG or 8-bit PNG)."""
+    import ctypes as C
+    lib = _abi.load_library()
+    w, h = C.c_int(0), C.c_int(0)
+    rc = lib.acmmp_read_image_bgr(path.encode(), None, 0, C.byref(w), C.byref(h))
+    if rc != _abi.ERR_ARG:
+        raise IOError(f"{path}: cannot decode image (status {rc})")
+    out = np.empty((h.value, w.value, 3), dtype=np.uint8)
+    rc = lib.acmmp_read_image_bgr(path.encode(), out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size, C.byref(w),
+                                  C.byref(h))
+    if rc != 0:
+        raise IOError(f"{path}: cannot decode image (status {rc})")
+    return out

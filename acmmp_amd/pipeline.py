@@ -154,3 +154,20 @@ def run_sequential(dense_folder: str, output_dir: str | None = None, device: int
             run_pass(True, False, False, g > 0)
         max_num_downscale -= 1
     return output_folder
+
+
+def run_fusion(dense_folder: str, output_folder: str, problems=None, geom_consistency: bool = True,
+               consistency_scalar: float = 0.3, num_consistent_thresh: int = 1, image_dir: str = "/images",
+               mask_folder: str = " ", write_debug_images: bool = False) -> int:
+    """RunFusion (src/acmmp_definitions.cpp:828-1043): writes
+    <output_folder>/ACMMP_model.ply; returns the number of fused points."""
+    if problems is None:
+        problems = generate_sample_list(dense_folder)
+    lib = _abi.load_library()
+    n = C.c_int(0)
+    rc = lib.acmmp_run_fusion(dense_folder.encode(), output_folder.encode(), _array(problems), len(problems),
+                              int(geom_consistency), float(consistency_scalar), int(num_consistent_thresh),
+                              image_dir.encode(), mask_folder.encode(), int(write_debug_images), C.byref(n))
+    if rc != 0:
+        raise AcmmpError(f"RunFusion failed (status {rc}): {lib.acmmp_fusion_last_error().decode()}")
+    return n.value

@@ -344,6 +344,19 @@ int acmmp_priors_available(const char *dense_folder, int num_cams);
 int acmmp_prior_plane_estimate(const char *dense_folder, int cam_num, const acmmp_camera *cam, int rows, int cols,
                                float *planes4);
 
+/* ~ RunFusion (src/acmmp_definitions.cpp:828-1043): fuse the depth_geom (or
+ * depth) + normal maps of all problems into <output>/ACMMP_model.ply (binary
+ * PLY of StoreColorPlyFileBinaryPointCloud, src/ACMMP.cpp:382-424), colours
+ * from <dense><image_dir>/%08d.jpg; optional masks <dense>/<mask_folder>/
+ * %08d.png (" " = none, as the reference); write_debug_images writes
+ * <dense>/approved_pixels_cam_%d.png. Sequential and literal (the
+ * reference's order dependence included). Host code. */
+int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const acmmp_problem *problems, int count,
+                     int geom_consistency, float consistency_scalar, int con_num_thresh, const char *image_dir,
+                     const char *mask_folder, int write_debug_images, int *num_points);
+/* Message of the last failing acmmp_run_fusion on this thread. */
+const char *acmmp_fusion_last_error(void);
+
 /* Message of the last failing driver call on this thread ("" when none). */
 const char *acmmp_pipeline_last_error(void);
 
@@ -365,6 +378,12 @@ float acmmp_depth_from_plane_param(const acmmp_camera *cam, const float *plane4,
  * Writes width*height floats (row-major) when capacity suffices; otherwise
  * returns ACMMP_ERR_ARG with *width / *height set. */
 int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *width, int *height);
+/* ~ cv::imread(path, cv::IMREAD_COLOR) as RunFusion uses it
+ * (src/acmmp_definitions.cpp:858): baseline JPEG decoded like libjpeg
+ * (fancy chroma upsampling, fixed-point YCbCr->RGB) or an 8-bit PNG;
+ * width*height*3 bytes in BGR order when capacity suffices, else
+ * ACMMP_ERR_ARG with the size set. */
+int acmmp_read_image_bgr(const char *path, uint8_t *out, size_t capacity, int *width, int *height);
 /* Image dimensions from the file header only (ComputeMultiScaleSettings,
  * src/acmmp_definitions.cpp:219-224, decodes the whole image for this). */
 int acmmp_image_size(const char *path, int *width, int *height);

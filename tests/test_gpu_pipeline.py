@@ -48,6 +48,7 @@ def test_cli_matches_in_process_driver(dense):
     exe = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
     r = subprocess.run([exe, dense, "--output_dir", "/CLI", "--quiet"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
+    assert os.path.getsize(os.path.join(dense + "/CLI", "ACMMP_model.ply")) > 1000  # RunFusion ran
     a, b = dense + "/ACMMP", dense + "/CLI"
     if not os.path.isdir(a):
         pipeline.run_sequential(dense, "/ACMMP")

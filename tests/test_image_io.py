@@ -108,3 +108,29 @@ def _resize_ref(src, dw, dh):
 def test_resize_linear(sw, sh, dw, dh):
     src = _texture(sw, sh, 9).astype(np.float32)
     np.testing.assert_array_equal(io.resize_linear(src, dw, dh), _resize_ref(src, dw, dh))
+
+
+@pytest.mark.parametrize("w,h,sub,q,rst", [
+    (64, 48, 0, 95, 0), (123, 77, 2, 90, 0), (200, 150, 1, 75, 0), (97, 131, 2, 100, 3), (41, 33, 2, 30, 1),
+    (2, 2, 2, 90, 0),
+])
+def test_jpeg_colour_bgr_matches_libjpeg(tmp_path, w, h, sub, q, rst):
+    """cv::imread(IMREAD_COLOR): libjpeg fancy upsampling + YCbCr tables."""
+    g = _texture(w, h, 3 * w + h)
+    rgb = np.stack([g, np.roll(g, 5, 0), 255 - np.roll(g, 2, 1)], -1)
+    path = str(tmp_path / "c.jpg")
+    kw = dict(quality=q, subsampling=sub)
+    if rst:
+        kw["restart_marker_blocks"] = rst
+    PIL.fromarray(rgb, "RGB").save(path, "JPEG", **kw)
+    ref = np.asarray(PIL.open(path).convert("RGB"))
+    np.testing.assert_array_equal(io.read_image_bgr(path), ref[..., ::-1])
+
+
+def test_gray_jpeg_as_bgr(tmp_path):
+    path = str(tmp_path / "g.jpg")
+    PIL.fromarray(_texture(30, 20, 1), "L").save(path, "JPEG", quality=80)
+    got = io.read_image_bgr(path)
+    ref = np.asarray(PIL.open(path))
+    for k in range(3):
+        np.testing.assert_array_equal(got[..., k], ref)
