@@ -199,6 +199,8 @@ SIGNATURES = {
     "acmmp_run_fusion": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int, C.c_float, C.c_int,
                                    C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)]),
     "acmmp_fusion_last_error": (C.c_char_p, []),
+    "acmmp_run_prior_aware_fusion": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int,
+                                               C.c_int, C.c_float, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "acmmp_priors_available": (C.c_int, [C.c_char_p, C.c_int]),
     "acmmp_prior_plane_estimate": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(Camera), C.c_int, C.c_int, _FP]),
     "acmmp_read_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint16), C.c_size_t, C.POINTER(C.c_int),

@@ -156,6 +156,86 @@ int store_ply(const std::string &path, const std::vector<Point> &pc) {  // Store
     return ACMMP_OK;
 }
 
+// ---- prior-aware fusion helpers (src/acmmp_definitions.cpp:443-571)
+struct CInfo {  // struct c_info
+    float dynamic_consistency = 0;
+    int x = 0, y = 0;
+    bool below_thresh = false;
+    int im_num = -1;
+};
+
+struct CMetric {  // struct cmetric
+    float reproj_err = 1e6, relative_depth_diff = 1e6, angle = 1e6;
+};
+
+struct FusionInputs {
+    std::vector<acmmp_camera> cameras;
+    std::vector<std::vector<float>> depths, normals, pdepths, pnormals;
+    std::vector<int> rows, cols;
+};
+
+CMetric metric_of(const FusionInputs &in, size_t i, int r, int c, float ref_depth, const float *ref_normal, int src,
+                  int src_r, int src_c, float src_depth, const float *src_normal) {
+    CMetric m;
+    if (src_depth > 0) {
+        const F3 tmp_X = world_point(src_c, src_r, src_depth, in.cameras[src]);
+        float tx, ty, proj_depth;
+        project(tmp_X, in.cameras[i], tx, ty, proj_depth);
+        m.reproj_err = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
+        m.relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
+        m.angle = get_angle(ref_normal, src_normal);
+    }
+    return m;
+}
+
+// get_consistency_metrics (:443-516)
+CInfo consistency_metrics(const FusionInputs &in, size_t i, int r, int c, float ref_depth, const float *ref_normal,
+                          int src, int src_r, int src_c) {
+    const size_t sp = (size_t)src_r * in.cols[src] + src_c;
+    const CMetric res0 = metric_of(in, i, r, c, ref_depth, ref_normal, src, src_r, src_c, in.depths[src][sp],
+                                   &in.normals[src][sp * 3]);
+    const CMetric res1 = metric_of(in, i, r, c, ref_depth, ref_normal, src, src_r, src_c, in.pdepths[src][sp],
+                                   &in.pnormals[src][sp * 3]);
+    const bool t0 = res0.reproj_err < 2.0f && res0.relative_depth_diff < 0.01f && res0.angle < 0.174533f;
+    const bool t1 = res1.reproj_err < 2.0f && res1.relative_depth_diff < 0.01f && res1.angle < 0.174533f;
+    CInfo out;
+    out.x = src_c;
+    out.y = src_r;
+    const float dc0 = std::exp(-(res0.reproj_err + 200 * res0.relative_depth_diff + res0.angle * 10));
+    const float dc1 = std::exp(-(res1.reproj_err + 200 * res1.relative_depth_diff + res1.angle * 10));
+    if (t0 && t1) {
+        out.dynamic_consistency = std::fmax(dc0, dc1);
+        out.below_thresh = true;
+        out.im_num = src;
+    } else if (t0) {
+        out.dynamic_consistency = dc0;
+        out.below_thresh = true;
+        out.im_num = src;
+    } else if (t1) {
+        out.dynamic_consistency = dc1;
+        out.below_thresh = true;
+        out.im_num = src;
+    }
+    return out;
+}
+
+// getCandidates (:520-571)
+void candidates(const FusionInputs &in, const std::vector<std::vector<uint8_t>> &masks, const std::vector<int> &srcs,
+                size_t i, int r, int c, float ref_depth, const float *ref_normal, std::vector<CInfo> &out) {
+    out.clear();
+    for (const int s : srcs) {
+        const F3 PointX = world_point(c, r, ref_depth, in.cameras[i]);
+        float px, py, proj_depth;
+        project(PointX, in.cameras[s], px, py, proj_depth);
+        const int src_r = int(py + 0.5f);
+        const int src_c = int(px + 0.5f);
+        if (src_c >= 0 && src_c < in.cols[s] && src_r >= 0 && src_r < in.rows[s]) {
+            if (masks[s][(size_t)src_r * in.cols[s] + src_c] == 1) continue;
+            out.push_back(consistency_metrics(in, i, r, c, ref_depth, ref_normal, s, src_r, src_c));
+        }
+    }
+}
+
 }  // namespace
 
 // in acmmp_pipeline.cpp (zlib PNG writer)
@@ -313,6 +393,151 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     }
     if (num_points) *num_points = (int)cloud.size();
     return store_ply(out + "/ACMMP_model.ply", cloud);
+}
+
+int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_folder, const char *fusion_folder,
+                                 const acmmp_problem *problems, int count, int geom_consistency,
+                                 float consistency_scalar, int num_consistent_thresh, int single_match_penalty,
+                                 int *num_points) {
+    if (!dense_folder || !output_folder || !fusion_folder || !problems || count <= 0)
+        return ffail(ACMMP_ERR_ARG, "bad args");
+    const std::string dense = dense_folder, out = output_folder, fus = fusion_folder;
+    const size_t n = (size_t)count;
+    FusionInputs in;
+    in.cameras.resize(n);
+    in.depths.resize(n);
+    in.normals.resize(n);
+    in.pdepths.resize(n);
+    in.pnormals.resize(n);
+    in.rows.resize(n);
+    in.cols.resize(n);
+    std::vector<std::vector<uint8_t>> images(n), masks(n);
+    std::map<int, int> image_id_2_index;
+    const char *suffix = geom_consistency ? "/depths_geom.dmb" : "/depths.dmb";
+    for (size_t i = 0; i < n; ++i) {
+        const int id = problems[i].ref_image_id;
+        image_id_2_index[id] = (int)i;
+        const std::string ipath = dense + "/images/" + id8(id) + ".jpg";
+        int iw = 0, ih = 0;
+        std::vector<uint8_t> img;
+        int rc = acmmp_read_image_bgr(ipath.c_str(), nullptr, 0, &iw, &ih);
+        if (rc == ACMMP_ERR_ARG) {
+            img.resize((size_t)iw * ih * 3);
+            rc = acmmp_read_image_bgr(ipath.c_str(), img.data(), img.size(), &iw, &ih);
+        }
+        if (rc) return ffail(rc, "cannot read image %s", ipath.c_str());
+        const std::string cpath = dense + "/cams/" + id8(id) + "_cam.txt";
+        if (acmmp_read_camera(cpath.c_str(), &in.cameras[i]))
+            return ffail(ACMMP_ERR_IO, "cannot read %s", cpath.c_str());
+        // maps of the other reconstruction (fusion_folder) and of this run's (output_folder) priors
+        const std::string rf = fus + "/2333_" + id8(id), pf = out + "/2333_" + id8(id);
+        int h, w, nb, h2, w2, nb2, h3, w3, nb3, h4, w4, nb4;
+        rc = read_dmb(rf + suffix, in.depths[i], h, w, nb);
+        if (!rc) rc = read_dmb(rf + "/normals.dmb", in.normals[i], h2, w2, nb2);
+        if (!rc) rc = read_dmb(pf + suffix, in.pdepths[i], h3, w3, nb3);
+        if (!rc) rc = read_dmb(pf + "/normals.dmb", in.pnormals[i], h4, w4, nb4);
+        if (rc) return rc;
+        if (nb != 1 || nb2 != 3 || nb3 != 1 || nb4 != 3 || h2 != h || w2 != w || h3 != h || w3 != w || h4 != h ||
+            w4 != w)
+            return ffail(ACMMP_ERR_IO, "map sizes of view %d disagree", id);
+        in.rows[i] = h;
+        in.cols[i] = w;
+        if (w == iw && h == ih) {
+            images[i] = std::move(img);
+        } else {
+            const float scale_x = w / static_cast<float>(iw);
+            const float scale_y = h / static_cast<float>(ih);
+            resize_u8(img, iw, ih, 3, images[i], w, h);
+            in.cameras[i].K[0] *= scale_x;
+            in.cameras[i].K[2] *= scale_x;
+            in.cameras[i].K[4] *= scale_y;
+            in.cameras[i].K[5] *= scale_y;
+        }
+        // mask files give 255/0 here (:654-661), never the 1 the checks test:
+        // only approvals mask pixels
+        masks[i].assign((size_t)w * h, 0);
+    }
+    std::vector<Point> cloud;
+    std::vector<CInfo> cand0, cand1;
+    for (size_t i = 0; i < n; ++i) {
+        const int W = in.cols[i], H = in.rows[i];
+        std::vector<int> srcs;
+        for (int j = 0; j < problems[i].num_src_images; ++j) {
+            auto it = image_id_2_index.find(problems[i].src_image_ids[j]);
+            if (it == image_id_2_index.end()) return ffail(ACMMP_ERR_ARG, "source is not a problem");
+            srcs.push_back(it->second);
+        }
+        for (int r = 0; r < H; ++r) {
+            for (int c = 0; c < W; ++c) {
+                const size_t pc = (size_t)r * W + c;
+                if (masks[i][pc] == 1) continue;
+                const float ref_depth = in.depths[i][pc], ref_p_depth = in.pdepths[i][pc];
+                const float *ref_normal = &in.normals[i][pc * 3], *ref_p_normal = &in.pnormals[i][pc * 3];
+                if (ref_depth <= 0.0 && ref_p_depth <= 0.0) continue;
+                float d_cons_0 = 0, d_cons_1 = 0;
+                int n0 = 0, n1 = 0;
+                bool t0 = false, t1 = false;
+                cand0.clear();
+                cand1.clear();
+                if (ref_depth > 0.0) {
+                    candidates(in, masks, srcs, i, r, c, ref_depth, ref_normal, cand0);
+                    for (const CInfo &k : cand0)
+                        if (k.below_thresh) {
+                            n0++;
+                            d_cons_0 += k.dynamic_consistency;
+                        }
+                    t0 = (n0 >= num_consistent_thresh) && (d_cons_0 > consistency_scalar * n0);
+                }
+                if (ref_p_depth > 0.0) {
+                    candidates(in, masks, srcs, i, r, c, ref_p_depth, ref_p_normal, cand1);
+                    for (const CInfo &k : cand1)
+                        if (k.below_thresh) {
+                            n1++;
+                            d_cons_1 += k.dynamic_consistency;
+                        }
+                    t1 = (n1 >= num_consistent_thresh) && (d_cons_1 > consistency_scalar * n1);
+                }
+                const std::vector<CInfo> *iter = nullptr;
+                bool passing = false;
+                float g_depth = 0;
+                const float *g_normal = ref_normal;
+                if (t0 && t1) {  // (:754-769)
+                    passing = true;
+                    if (n1 >= n0) {
+                        iter = &cand1;
+                        g_depth = ref_p_depth;
+                        g_normal = ref_p_normal;
+                    } else {
+                        iter = &cand0;
+                        g_depth = ref_depth;
+                        g_normal = ref_normal;
+                    }
+                } else if (t1) {
+                    passing = n1 >= (num_consistent_thresh + single_match_penalty);
+                    iter = &cand1;
+                    g_depth = ref_p_depth;
+                    g_normal = ref_p_normal;
+                } else {
+                    passing = t0 && n0 >= (num_consistent_thresh + single_match_penalty);
+                    iter = &cand0;
+                    g_depth = ref_depth;
+                    g_normal = ref_normal;
+                }
+                if (passing) {
+                    Point p;
+                    p.coord = world_point(c, r, g_depth, in.cameras[i]);
+                    p.normal = F3{g_normal[0], g_normal[1], g_normal[2]};
+                    const uint8_t *bgr = &images[i][pc * 3];
+                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
+                    cloud.push_back(p);
+                    for (const CInfo &k : *iter)
+                        if (k.below_thresh) masks[k.im_num][(size_t)k.y * in.cols[k.im_num] + k.x] = 1;
+                }
+            }
+        }
+    }
+    if (num_points) *num_points = (int)cloud.size();
+    return store_ply(out + "/ACMMP_prior_model.ply", cloud);
 }
 
 }  // extern "C"

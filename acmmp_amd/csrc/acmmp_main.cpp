@@ -5,9 +5,10 @@
 // (the reference's Gauss-Seidel schedule). No GUI calls.
 //
 // After the passes it fuses the maps like main_ACMMP (:178-199) with the
-// library's RunFusion port (acmmp_fusion.cpp) into <out>/ACMMP_model.ply;
-// RunPriorAwareFusion (--multi_fusion with -p, or --force_fusion) is not
-// ported: the maps are written and the reference's fuse_data can be used.
+// library's ports (acmmp_fusion.cpp): RunFusion into <out>/ACMMP_model.ply, or
+// with -p --multi_fusion [DIR] / --force_fusion RunPriorAwareFusion against
+// the reconstruction in <dense>DIR (default /ACMMP) into
+// <out>/ACMMP_prior_model.ply.
 #include <sys/stat.h>
 
 #include <cmath>
@@ -36,7 +37,9 @@ void usage() {
         "  --mask_dir DIR           boolean masks (0, 255) under <dense>/DIR\n"
         "  --image_override DIR     texture images for fusion (default /images)\n"
         "  --no_fusion              stop after the depth/normal/cost maps\n"
-        "  --multi_fusion / --force_fusion / --single_match_penalty: prior-aware fusion (not ported)\n");
+        "  --multi_fusion [DIR]     with -p: prior-aware fusion against <dense>DIR (default /ACMMP)\n"
+        "  --force_fusion           prior-aware fusion even without -p\n"
+        "  --single_match_penalty N extra consistent views required of one-sided support (0)\n");
 }
 
 int die(const char *what) {
@@ -47,11 +50,11 @@ int die(const char *what) {
 }  // namespace
 
 int main(int argc, char **argv) {
-    std::string dense_folder, output_dir = "/ACMMP", mask_dir = " ", image_dir = "/images";
+    std::string dense_folder, output_dir = "/ACMMP", mask_dir = " ", image_dir = "/images", fusion_dir = "/ACMMP";
     bool prior = false, quiet = false, triangulation = true, renamed_outdir = false, fusion = true;
     bool multi_fusion = false, force_fusion = false;
     float consistency_scalar = 0.3f;
-    int num_consistent_thresh = 1;
+    int num_consistent_thresh = 1, single_match_penalty = 0;
     int device = 0, iterations = 0;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
@@ -90,12 +93,12 @@ int main(int argc, char **argv) {
         } else if (a == "--image_override") {
             image_dir = value();
         } else if (a == "--single_match_penalty") {
-            value();
+            single_match_penalty = std::atoi(value().c_str());
         } else if (a == "--no_fusion") {
             fusion = false;
         } else if (a == "--multi_fusion") {
             multi_fusion = true;
-            if (i + 1 < argc && argv[i + 1][0] != '-') ++i;
+            if (i + 1 < argc && argv[i + 1][0] != '-') fusion_dir = argv[++i];
         } else if (a == "--force_fusion") {
             force_fusion = true;
         } else if (!a.empty() && a[0] != '-' && dense_folder.empty()) {
@@ -179,12 +182,18 @@ int main(int argc, char **argv) {
         max_num_downscale--;
     }
     if (!fusion) return 0;
+    int npts = 0;
     if ((prior && multi_fusion) || force_fusion) {
-        std::printf("Prior-aware fusion is not ported; maps are under %s for the reference's fuse_data\n",
-                    output_folder.c_str());
+        const std::string fusion_folder = dense_folder + fusion_dir;
+        if (acmmp_run_prior_aware_fusion(dense_folder.c_str(), output_folder.c_str(), fusion_folder.c_str(),
+                                         problems.data(), num_images, 1, consistency_scalar, num_consistent_thresh,
+                                         single_match_penalty, &npts)) {
+            std::fprintf(stderr, "acmmp_main: RunPriorAwareFusion: %s\n", acmmp_fusion_last_error());
+            return 1;
+        }
+        if (!quiet) std::printf("Fused %d points into %s/ACMMP_prior_model.ply\n", npts, output_folder.c_str());
         return 0;
     }
-    int npts = 0;
     if (acmmp_run_fusion(dense_folder.c_str(), output_folder.c_str(), problems.data(), num_images, 1,
                          consistency_scalar, num_consistent_thresh, image_dir.c_str(), mask_dir.c_str(), 1, &npts)) {
         std::fprintf(stderr, "acmmp_main: RunFusion: %s\n", acmmp_fusion_last_error());

@@ -171,3 +171,21 @@ def run_fusion(dense_folder: str, output_folder: str, problems=None, geom_consis
     if rc != 0:
         raise AcmmpError(f"RunFusion failed (status {rc}): {lib.acmmp_fusion_last_error().decode()}")
     return n.value
+
+
+def run_prior_aware_fusion(dense_folder: str, output_folder: str, fusion_folder: str, problems=None,
+                           geom_consistency: bool = True, consistency_scalar: float = 0.3,
+                           num_consistent_thresh: int = 1, single_match_penalty: int = 0) -> int:
+    """RunPriorAwareFusion (src/acmmp_definitions.cpp:573-826): writes
+    <output_folder>/ACMMP_prior_model.ply; returns the number of points."""
+    if problems is None:
+        problems = generate_sample_list(dense_folder)
+    lib = _abi.load_library()
+    n = C.c_int(0)
+    rc = lib.acmmp_run_prior_aware_fusion(dense_folder.encode(), output_folder.encode(), fusion_folder.encode(),
+                                          _array(problems), len(problems), int(geom_consistency),
+                                          float(consistency_scalar), int(num_consistent_thresh),
+                                          int(single_match_penalty), C.byref(n))
+    if rc != 0:
+        raise AcmmpError(f"RunPriorAwareFusion failed (status {rc}): {lib.acmmp_fusion_last_error().decode()}")
+    return n.value

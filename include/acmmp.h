@@ -354,7 +354,16 @@ int acmmp_prior_plane_estimate(const char *dense_folder, int cam_num, const acmm
 int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const acmmp_problem *problems, int count,
                      int geom_consistency, float consistency_scalar, int con_num_thresh, const char *image_dir,
                      const char *mask_folder, int write_debug_images, int *num_points);
-/* Message of the last failing acmmp_run_fusion on this thread. */
+/* ~ RunPriorAwareFusion (src/acmmp_definitions.cpp:573-826): fuses the maps
+ * of `fusion_folder` with this run's (`output_folder`) seeded maps as priors,
+ * per pixel choosing the hypothesis with more consistent views
+ * (single_match_penalty for one-sided support), into
+ * <output>/ACMMP_prior_model.ply. Host code, literal. */
+int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_folder, const char *fusion_folder,
+                                 const acmmp_problem *problems, int count, int geom_consistency,
+                                 float consistency_scalar, int num_consistent_thresh, int single_match_penalty,
+                                 int *num_points);
+/* Message of the last failing acmmp_run_fusion / _prior_aware_fusion on this thread. */
 const char *acmmp_fusion_last_error(void);
 
 /* Message of the last failing driver call on this thread ("" when none). */

@@ -121,3 +121,107 @@ def read_ply(path):
     rec = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
                     ("r", "u1"), ("g", "u1"), ("b", "u1")])
     return np.frombuffer(body, dtype=rec, count=n)
+
+
+def _metric(i, r, c, ref_depth, ref_normal, cams, s, src_r, src_c, src_depth, src_normal):
+    if not src_depth > 0:
+        return (f32(1e6), f32(1e6), f32(1e6))
+    tX = _world(src_c, src_r, src_depth, cams[s])
+    tx, ty, proj_depth = _project(tX, cams[i])
+    reproj = f32(math.sqrt(float(f32(c) - tx) ** 2 + float(f32(r) - ty) ** 2))
+    rel = abs(proj_depth - ref_depth) / ref_depth
+    return (reproj, rel, _angle(ref_normal, src_normal))
+
+
+def _cmetrics(i, r, c, ref_depth, ref_normal, cams, s, src_r, src_c, maps):
+    depths, normals, pdepths, pnormals = maps
+    res = [_metric(i, r, c, ref_depth, ref_normal, cams, s, src_r, src_c, f32(d[s][src_r, src_c]),
+                   [f32(v) for v in nn[s][src_r, src_c]]) for d, nn in ((depths, normals), (pdepths, pnormals))]
+    th = [m[0] < 2.0 and m[1] < f32(0.01) and m[2] < f32(0.174533) for m in res]
+    dc = [f32(_libm.expf(float(-(m[0] + f32(200) * m[1] + m[2] * f32(10))))) for m in res]
+    if th[0] and th[1]:
+        return (max(dc[0], dc[1]), src_c, src_r, True, s)
+    if th[0]:
+        return (dc[0], src_c, src_r, True, s)
+    if th[1]:
+        return (dc[1], src_c, src_r, True, s)
+    return (f32(0), src_c, src_r, False, -1)
+
+
+def run_prior_aware_fusion(dense, out, fusion_folder, geom=True, consistency_scalar=0.3, con_num_thresh=1,
+                           penalty=0):
+    """RunPriorAwareFusion (src/acmmp_definitions.cpp:573-826) restated."""
+    from PIL import Image
+    problems = aio.read_pair(os.path.join(dense, "pair.txt"))
+    index = {p.ref_image_id: i for i, p in enumerate(problems)}
+    suffix = "depths_geom.dmb" if geom else "depths.dmb"
+    imgs, cams, depths, normals, pdepths, pnormals, masks = [], [], [], [], [], [], []
+    for p in problems:
+        rgb = np.asarray(Image.open(os.path.join(dense, "images", "%08d.jpg" % p.ref_image_id)).convert("RGB"))
+        imgs.append(rgb[..., ::-1])
+        cams.append(aio.read_camera(os.path.join(dense, "cams", "%08d_cam.txt" % p.ref_image_id)))
+        rf, pf = aio.result_folder(fusion_folder, p.ref_image_id), aio.result_folder(out, p.ref_image_id)
+        depths.append(aio.read_dmb(os.path.join(rf, suffix)))
+        normals.append(aio.read_dmb(os.path.join(rf, "normals.dmb")))
+        pdepths.append(aio.read_dmb(os.path.join(pf, suffix)))
+        pnormals.append(aio.read_dmb(os.path.join(pf, "normals.dmb")))
+        masks.append(np.zeros(depths[-1].shape, np.uint8))
+    maps = (depths, normals, pdepths, pnormals)
+    cloud = []
+    for i, p in enumerate(problems):
+        H, W = depths[i].shape
+        srcs = [index[s] for s in p.src_image_ids]
+
+        def cands(r, c, ref_depth, ref_normal):
+            out_c = []
+            for s in srcs:
+                sh, sw = depths[s].shape
+                X = _world(c, r, ref_depth, cams[i])
+                px, py, _ = _project(X, cams[s])
+                src_r, src_c = int(py + f32(0.5)), int(px + f32(0.5))
+                if 0 <= src_c < sw and 0 <= src_r < sh:
+                    if masks[s][src_r, src_c] == 1:
+                        continue
+                    out_c.append(_cmetrics(i, r, c, ref_depth, ref_normal, cams, s, src_r, src_c, maps))
+            return out_c
+
+        for r in range(H):
+            for c in range(W):
+                if masks[i][r, c] == 1:
+                    continue
+                rd, rpd = f32(depths[i][r, c]), f32(pdepths[i][r, c])
+                rn = [f32(v) for v in normals[i][r, c]]
+                rpn = [f32(v) for v in pnormals[i][r, c]]
+                if rd <= 0.0 and rpd <= 0.0:
+                    continue
+                c0, c1, n0, n1, d0, d1, t0, t1 = [], [], 0, 0, f32(0), f32(0), False, False
+                if rd > 0.0:
+                    c0 = cands(r, c, rd, rn)
+                    for k in c0:
+                        if k[3]:
+                            n0 += 1
+                            d0 = d0 + k[0]
+                    t0 = n0 >= con_num_thresh and d0 > f32(consistency_scalar) * f32(n0)
+                if rpd > 0.0:
+                    c1 = cands(r, c, rpd, rpn)
+                    for k in c1:
+                        if k[3]:
+                            n1 += 1
+                            d1 = d1 + k[0]
+                    t1 = n1 >= con_num_thresh and d1 > f32(consistency_scalar) * f32(n1)
+                if t0 and t1:
+                    passing = True
+                    it, gd, gn = (c1, rpd, rpn) if n1 >= n0 else (c0, rd, rn)
+                elif t1:
+                    passing = n1 >= con_num_thresh + penalty
+                    it, gd, gn = c1, rpd, rpn
+                else:
+                    passing = t0 and n0 >= con_num_thresh + penalty
+                    it, gd, gn = c0, rd, rn
+                if passing:
+                    b, g, rr = (int(v) for v in imgs[i][r, c])
+                    cloud.append((_world(c, r, gd, cams[i]), gn, (rr, g, b)))
+                    for k in it:
+                        if k[3]:
+                            masks[k[4]][k[2], k[1]] = 1
+    return cloud

@@ -58,3 +58,36 @@ def test_fusion_thresholds_reduce_points(tmp_path):
     n2 = pipeline.run_fusion(d, out, num_consistent_thresh=2)
     n3 = pipeline.run_fusion(d, out, consistency_scalar=0.9)
     assert n1 > n2 > 0 and n1 > n3
+
+
+def _compare_cloud(ply, ref):
+    assert len(ply) == len(ref)
+    xyz = np.array([p[0] for p in ref], np.float32).reshape(-1, 3)
+    nrm = np.array([p[1] for p in ref], np.float32).reshape(-1, 3)
+    col = np.array([p[2] for p in ref], np.uint8).reshape(-1, 3)
+    np.testing.assert_array_equal(np.stack([ply["x"], ply["y"], ply["z"]], -1).view(np.uint32), xyz.view(np.uint32))
+    np.testing.assert_array_equal(np.stack([ply["nx"], ply["ny"], ply["nz"]], -1).view(np.uint32),
+                                  nrm.view(np.uint32))
+    np.testing.assert_array_equal(np.stack([ply["r"], ply["g"], ply["b"]], -1), col)
+
+
+def test_prior_aware_fusion_matches_python_restatement(tmp_path):
+    from oracle_fusion import run_prior_aware_fusion
+    d, out = _dense_with_maps(tmp_path)
+    # a second reconstruction (the "prior" run's output folder) with perturbed maps
+    prior = d + "/ACMMP_PRIOR"
+    rng = np.random.default_rng(2)
+    for i in range(4):
+        src, dst = aio.result_folder(out, i), aio.result_folder(prior, i)
+        os.makedirs(dst, exist_ok=True)
+        dep = aio.read_dmb(os.path.join(src, "depths_geom.dmb"))
+        dep = np.where(rng.random(dep.shape) < 0.3, dep * 1.05, dep).astype(np.float32)
+        dep[rng.random(dep.shape) < 0.1] = 0.0
+        aio.write_dmb(os.path.join(dst, "depths_geom.dmb"), dep)
+        aio.write_dmb(os.path.join(dst, "normals.dmb"), aio.read_dmb(os.path.join(src, "normals.dmb")))
+    for penalty in (0, 1):
+        n = pipeline.run_prior_aware_fusion(d, prior, out, single_match_penalty=penalty)
+        ply = read_ply(os.path.join(prior, "ACMMP_prior_model.ply"))
+        ref = run_prior_aware_fusion(d, prior, out, penalty=penalty)
+        assert n > 500
+        _compare_cloud(ply, ref)
