@@ -765,17 +765,6 @@ int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checke
     return rc;
 }
 
-#ifdef ACMMP_DIAG_PROBE
-// Diagnostic builds only: split-kernel NCC throughput probe on the current state.
-int acmmp_diag_probe(acmmp_ctx *ctx, int variant, int reps, float *ms) {
-    int rc = check_ready(ctx);
-    if (rc) return rc;
-    rc = kv_upload(ctx);
-    if (rc) return rc;
-    return probe_run(ctx->d_kv, ctx->h_kv, state_of(ctx), variant, reps, ms, ctx->stream);
-}
-#endif
-
 // Diagnostic builds only (ACMMP_DIAG_STAMPS); not declared in include/acmmp.h.
 int acmmp_diag_read_cycles(uint64_t *out8) {
     return out8 ? diag_read_cycles((unsigned long long *)out8) : ACMMP_ERR_ARG;

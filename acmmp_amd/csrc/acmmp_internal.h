@@ -85,8 +85,6 @@ hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4
 hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch,
                             hipStream_t stream);
 int diag_read_cycles(unsigned long long *out8);
-int probe_run(const KViews *d_kv, const KViews &h_kv, const KState &st, int variant, int reps, float *ms,
-              hipStream_t s);
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);

@@ -38,7 +38,6 @@ constexpr int kTaps = 6;
 #ifndef ACMMP_SWEEP_WAVES
 #define ACMMP_SWEEP_WAVES 2
 #endif
-constexpr int kSamples = kTaps * kTaps;
 
 // ----------------------------------------------------------------- textures
 DEV float texel(const float *img, int pitch, int W, int H, int x, int y) {
@@ -319,35 +318,29 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // the 36 bilateral weights (ComputeBilateralWeight :353-358) and the
 // normalised ref mean / variance — identical for all 14*(N-1) calls of a
 // pixel-iteration, so computed once (same operations, same order).
-// LDS slot of patch sample (column ii, row jj): in the order the gathers
-// visit them (rows outer), so consecutive reads are adjacent (ds_read2st64).
-DEV int widx(int ii, int jj) { return jj * kTaps + ii; }
-
-// LDS slot per patch sample: (w, w * ref) pairs (ACMMP_LDS_WR=1, 72 KB per
-// block, no per-sample multiply) or w alone (0, 36 KB per block: leaves room
-// for more resident blocks; w * ref is then formed from the ref tile).
-#ifndef ACMMP_LDS_WR
-#define ACMMP_LDS_WR 1
-#endif
-#if ACMMP_LDS_WR
-typedef float2 WSlot;
-#else
-typedef float WSlot;
-#endif
+//
+// The source side of the NCC runs on PAIRS of patch columns (2p, 2p+1) held
+// as packed-FP32 lanes (SoA): one v_pk_* instruction does the same IEEE
+// operation for both samples of a pair, and the pair's weights come from LDS
+// as one float4 (w_a, w_b, w_a*ref_a, w_b*ref_b), so no register shuffling is
+// needed to feed the packed ops. LDS slot of (column pair p, patch row jj):
+// jj * 3 + p, in the order the row loop reads them.
+constexpr int kPairs = kTaps / 2;
+constexpr int kSlots = kPairs * kTaps;
+DEV int wslot(int p, int jj) { return jj * kPairs + p; }
 
 struct PixPatch {
-    WSlot *w;        // LDS: slot of sample k of this lane at [k * kThreads]
+    float4 *w;       // LDS: slot k of this lane at [k * kThreads]
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
     float inv_wsum;  // inv_bilateral_weight_sum
 };
 
-// The 36 weights live in LDS with their products w * ref (the reference
-// half of every NCC term is view-invariant), one 256-pair row per sample
-// index k, so a wave's read of sample k is one conflict-free ds_read_b64 and
-// costs no VGPRs: 72 KB + the 3.9 KB tile per 256-thread block (2 blocks =
-// the 8 waves of a CU at this kernel's occupancy).
+// 18 float4 rows of 256 lanes: 72 KB + the 3.9 KB tile per 256-thread block
+// (2 blocks = the 8 waves of a CU at this kernel's occupancy). A wave's read
+// of one slot is a conflict-free ds_read_b128 and costs no VGPRs between
+// NCC calls.
 constexpr int kThreads = kBX * kBY;
 
 DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
@@ -372,11 +365,9 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_ref += wr;
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
-#if ACMMP_LDS_WR
-            pp.w[widx(ii, jj) * kThreads] = make_float2(w, wr);
-#else
-            pp.w[widx(ii, jj) * kThreads] = w;
-#endif
+            float *slot = reinterpret_cast<float *>(&pp.w[wslot(ii >> 1, jj) * kThreads]);
+            slot[ii & 1] = w;
+            slot[2 + (ii & 1)] = wr;
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -390,15 +381,6 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
     pp.inv_wsum = inv;
 }
 
-// Fetch stage of one patch column (fixed x = px - 5 + 2 ii) of the source
-// samples: projection (pin P1, the x-term hoisted per column), the coordinate
-// clamp of pin P2, and ONE 16-byte load per sample of the 2x2 bilinear
-// footprint from the row-paired padded image (element (r, c) holds the
-// texels of rows r-1 and r at column c-1, clamp-to-edge, so the load at
-// (y0 + 1, x0 + 1) returns (t00, t01, t10, t11) = texels (x0,y0), (x0,y0+1),
-// (x0+1,y0), (x0+1,y0+1)). The x/y halves of the projection and of the
-// coordinate arithmetic run as packed-FP32 pairs (v_pk_fma / v_pk_mul /
-// v_pk_add: the same IEEE operation per component as the scalar pin).
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -407,152 +389,127 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ u32x4 amdgcn_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                 int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
 
-struct ColFetch {
-    u32x4 t[kTaps];               // (t00, t01, t10, t11) per sample
-    float ax[kTaps], ay[kTaps];   // bilinear weights
-};
-
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+DEV f2v splat(float v) { return f2v{v, v}; }
 
-template <bool FAST>
-DEV void fetch_column(const SrcImage &im, const float *H, float x, int py, ColFetch &f) {
-    const f2v cxy = fma2(f2v{H[0], H[3]}, f2v{x, x}, f2v{H[2], H[5]});
-    const float cz = dm_fma(H[6], x, H[8]);
-    const f2v h14 = f2v{H[1], H[4]};
-    const float fw = (float)im.W, fh = (float)im.H;
-#pragma unroll
-    for (int jj = 0; jj < kTaps; ++jj) {
-        const float y = (float)(py - 5 + 2 * jj);
-        const f2v hxy = fma2(h14, f2v{y, y}, cxy);
-        const float hz = dm_fma(H[7], y, cz);
-        const float inv = recip<FAST>(hz);
-        f2v uv = hxy * f2v{inv, inv};
-        uv = (uv + 0.5f) - 0.5f;
-        // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
-        // (finite homography, |hz| inside the reciprocal window), where
-        // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
-        // bounds are never +-0) == the oracle's selects.
-        const float xs = FAST ? __builtin_amdgcn_fmed3f(uv.x, -1.0f, fw) : fminf(fmaxf(uv.x, -1.0f), fw);
-        const float ys = FAST ? __builtin_amdgcn_fmed3f(uv.y, -1.0f, fh) : fminf(fmaxf(uv.y, -1.0f), fh);
-        const f2v fl = f2v{dm_floor(xs), dm_floor(ys)};
-        const f2v a = f2v{xs, ys} - fl;
-        f.ax[jj] = a.x;
-        f.ay[jj] = a.y;
-        // record index (y0 + 1) * pitch + x0 + 1 = fma(y0, pitch, x0 + pitch + 1):
-        // integers below 2^24, so exact in fp32 (checked on the host)
-        const unsigned idx = (unsigned)dm_fma(fl.y, im.fpitch, fl.x + im.fp1);
-        f.t[jj] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)idx, 0, 0, 0);
-    }
-}
-
-// Bilinear value of a fetched sample (pin P2's lerp order):
-// top = fma(ax, t10 - t00, t00), bot = fma(ax, t11 - t01, t01) as one packed
-// pair, then fma(ay, bot - top, top).
-DEV float bilinear_sample(const ColFetch &f, int jj) {
-    const u32x4 t = f.t[jj];
+// Bilinear value of one fetched sample t = (t00, t01, t10, t11) (pin P2's
+// lerp order): top = fma(ax, t10 - t00, t00), bot = fma(ax, t11 - t01, t01)
+// as one packed pair, then fma(ay, bot - top, top).
+DEV float lerp_sample(u32x4 t, float ax, float ay) {
     const f2v lo = f2v{__uint_as_float(t.x), __uint_as_float(t.y)};
     const f2v hi = f2v{__uint_as_float(t.z), __uint_as_float(t.w)};
-    const f2v tb = fma2(f2v{f.ax[jj], f.ax[jj]}, hi - lo, lo);
-    return dm_fma(f.ay[jj], tb.y - tb.x, tb.x);
+    const f2v tb = fma2(splat(ax), hi - lo, lo);
+    return dm_fma(ay, tb.y - tb.x, tb.x);
 }
 
-// Row-order gathers: the 6 samples of one patch row (fixed y) of a lane sit
-// in the same one or two cache lines of the row-paired image, so issuing the
-// patch row by row keeps each wave's working set at ~64 lines between reuses
-// (column order touches 6 lines per lane before coming back) — what matters
-// when the hypotheses of neighbouring lanes are incoherent (early
-// iterations). The per-column projection terms are hoisted.
-struct ColTerms {
-    f2v cxy[kTaps];   // (fma(H0, x, H2), fma(H3, x, H5)) per patch column
-    float cz[kTaps];  // fma(H6, x, H8)
-};
-
+// Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412).
+//
+// Per sample: projection (pin P1, the x-terms hoisted per column), the
+// coordinate clamp of pin P2, and ONE 16-byte load of the 2x2 bilinear
+// footprint from the row-paired padded image (element (r, c) holds the
+// texels of rows r-1 and r at column c-1, clamp-to-edge, so the load at
+// (y0 + 1, x0 + 1) returns texels (x0,y0), (x0,y0+1), (x0+1,y0), (x0+1,y0+1)).
+//
+// Rows are gathered one at a time (a lane's 6 samples of a row sit in the
+// same one or two cache lines, which matters when neighbouring lanes'
+// hypotheses are incoherent) and accumulated into per-column partial sums:
+// within a column the rows are still added in order jj = 0..5, columns are
+// summed at the end in order ii — the pinned order (src/ACMMP.cu:382-412).
 template <bool FAST>
-DEV void fetch_row(const SrcImage &im, const float *H, const ColTerms &ct, int py, int jj, ColFetch &f) {
-    const f2v h14 = f2v{H[1], H[4]};
-    const float fw = (float)im.W, fh = (float)im.H;
-    const float y = (float)(py - 5 + 2 * jj);
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int wstride, int px, int py,
+                       float &sum_src, float &sum_ss, float &sum_rs) {
+    f2v cx[kPairs], cy[kPairs], cz[kPairs];
 #pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-        const f2v hxy = fma2(h14, f2v{y, y}, ct.cxy[ii]);
-        const float hz = dm_fma(H[7], y, ct.cz[ii]);
-        const float inv = recip<FAST>(hz);
-        f2v uv = hxy * f2v{inv, inv};
-        uv = (uv + 0.5f) - 0.5f;
-        const float xs = FAST ? __builtin_amdgcn_fmed3f(uv.x, -1.0f, fw) : fminf(fmaxf(uv.x, -1.0f), fw);
-        const float ys = FAST ? __builtin_amdgcn_fmed3f(uv.y, -1.0f, fh) : fminf(fmaxf(uv.y, -1.0f), fh);
-        const f2v fl = f2v{dm_floor(xs), dm_floor(ys)};
-        const f2v a = f2v{xs, ys} - fl;
-        f.ax[ii] = a.x;
-        f.ay[ii] = a.y;
-        const unsigned idx = (unsigned)dm_fma(fl.y, im.fpitch, fl.x + im.fp1);
-        f.t[ii] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)idx, 0, 0, 0);
+    for (int p = 0; p < kPairs; ++p) {
+        const f2v x = f2v{(float)(px - 5 + 4 * p), (float)(px - 3 + 4 * p)};
+        cx[p] = fma2(splat(H[0]), x, splat(H[2]));
+        cy[p] = fma2(splat(H[3]), x, splat(H[5]));
+        cz[p] = fma2(splat(H[6]), x, splat(H[8]));
     }
-}
-
-template <bool FAST>
-DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, int wstride, const float *tile, int tb,
-                       int px, int py, float &sum_src, float &sum_ss, float &sum_rs) {
-    ColTerms ct;
+    f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
 #pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-        const float x = (float)(px - 5 + 2 * ii);
-        ct.cxy[ii] = fma2(f2v{H[0], H[3]}, f2v{x, x}, f2v{H[2], H[5]});
-        ct.cz[ii] = dm_fma(H[6], x, H[8]);
-    }
-    // per-column partial sums, accumulated row by row: within a column the
-    // rows are still added in order jj = 0..5 (the pinned order,
-    // src/ACMMP.cu:382-412), columns are summed at the end in order ii
-    float r_s[kTaps];
-    f2v racc[kTaps];
-#pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-        r_s[ii] = 0.0f;
-        racc[ii] = f2v{0.0f, 0.0f};
-    }
+    for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
+    const f2v fw = splat((float)im.W), fh = splat((float)im.H);
     // rows are a rolled loop: one row's 6 gathers in flight, reduced, next row
     // (unrolling lets the compiler hoist every row's address math and spill)
 #pragma unroll 1
     for (int jj = 0; jj < kTaps; ++jj) {
-        ColFetch f;
-        fetch_row<FAST>(im, H, ct, py, jj, f);
+        const f2v y = splat((float)(py - 5 + 2 * jj));
+        u32x4 t[kTaps];
+        f2v ax[kPairs], ay[kPairs];
 #pragma unroll
-        for (int ii = 0; ii < kTaps; ++ii) {
-            const float sv = bilinear_sample(f, ii);
-#if ACMMP_LDS_WR
-            const float2 w = wl[widx(ii, jj) * wstride];
-#else
-            const float wv = wl[widx(ii, jj) * wstride];
-            const float2 w = make_float2(wv, wv * tile[tb + ii + 2 * kTileW * jj]);
-#endif
-            const float ws = w.x * sv;
-            r_s[ii] += ws;
-            racc[ii] = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc[ii]);
+        for (int p = 0; p < kPairs; ++p) {
+            const f2v hx = fma2(splat(H[1]), y, cx[p]);
+            const f2v hy = fma2(splat(H[4]), y, cy[p]);
+            const f2v hz = fma2(splat(H[7]), y, cz[p]);
+            f2v inv;
+            if (FAST) {  // v_rcp + one Newton step == IEEE 1/z in the window
+                const f2v r = f2v{__builtin_amdgcn_rcpf(hz.x), __builtin_amdgcn_rcpf(hz.y)};
+                inv = fma2(fma2(-hz, r, splat(1.0f)), r, r);
+            } else {
+                inv = f2v{1.0f / hz.x, 1.0f / hz.y};
+            }
+            f2v u = hx * inv, v = hy * inv;
+            u = (u + 0.5f) - 0.5f;
+            v = (v + 0.5f) - 0.5f;
+            // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
+            // (finite homography, |hz| inside the reciprocal window), where
+            // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
+            // bounds are never +-0) == the oracle's selects.
+            f2v xs, ys;
+            if (FAST) {
+                xs = f2v{__builtin_amdgcn_fmed3f(u.x, -1.0f, fw.x), __builtin_amdgcn_fmed3f(u.y, -1.0f, fw.x)};
+                ys = f2v{__builtin_amdgcn_fmed3f(v.x, -1.0f, fh.x), __builtin_amdgcn_fmed3f(v.y, -1.0f, fh.x)};
+            } else {
+                xs = f2v{fminf(fmaxf(u.x, -1.0f), fw.x), fminf(fmaxf(u.y, -1.0f), fw.x)};
+                ys = f2v{fminf(fmaxf(v.x, -1.0f), fh.x), fminf(fmaxf(v.y, -1.0f), fh.x)};
+            }
+            const f2v flx = f2v{dm_floor(xs.x), dm_floor(xs.y)};
+            const f2v fly = f2v{dm_floor(ys.x), dm_floor(ys.y)};
+            ax[p] = xs - flx;
+            ay[p] = ys - fly;
+            // record index (y0 + 1) * pitch + x0 + 1 = fma(y0, pitch, x0 + pitch + 1):
+            // integers below 2^24, so exact in fp32 (checked on the host)
+            const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
+            t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)(unsigned)idx.x, 0, 0, 0);
+            t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)(unsigned)idx.y, 0, 0, 0);
+        }
+#pragma unroll
+        for (int p = 0; p < kPairs; ++p) {
+            const f2v sv = f2v{lerp_sample(t[2 * p], ax[p].x, ay[p].x), lerp_sample(t[2 * p + 1], ax[p].y, ay[p].y)};
+            const float4 w = wl[wslot(p, jj) * wstride];
+            const f2v ws = f2v{w.x, w.y} * sv;
+            acc_s[p] += ws;
+            acc_ss[p] = fma2(ws, sv, acc_ss[p]);
+            acc_rs[p] = fma2(f2v{w.z, w.w}, sv, acc_rs[p]);
         }
     }
     sum_src = 0.0f;
     sum_ss = 0.0f;
     sum_rs = 0.0f;
 #pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-        sum_src += r_s[ii];
-        sum_ss += racc[ii].x;
-        sum_rs += racc[ii].y;
+    for (int p = 0; p < kPairs; ++p) {
+        sum_src += acc_s[p].x;
+        sum_src += acc_s[p].y;
+        sum_ss += acc_ss[p].x;
+        sum_ss += acc_ss[p].y;
+        sum_rs += acc_rs[p].x;
+        sum_rs += acc_rs[p].y;
     }
 }
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // returns the three weighted sums (ncc_sums_rows above).
 template <bool FAST>
-DEV void ncc_sums(const SrcImage &im, const float *H, const float *tile, int tb, const PixPatch &pp, int px,
-                  int py, float &sum_src, float &sum_ss, float &sum_rs) {
+DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
+                  float &sum_ss, float &sum_rs) {
     // re-read weights from LDS each call rather than caching them in VGPRs
     // (launder the integer offset, not the pointer, so the LDS address space
     // stays visible and the reads are ds_read, not flat)
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
-    const WSlot *wl = pp.w - pp.wo + wo;
-    ncc_sums_rows<FAST>(im, H, wl, kThreads, tile, tb, px, py, sum_src, sum_ss, sum_rs);
+    const float4 *wl = pp.w - pp.wo + wo;
+    ncc_sums_rows<FAST>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
@@ -570,9 +527,6 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     homography(kv, v, h, H);
     const float2 pt = project(H, (float)px, (float)py);
     if (pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f) return cost_max;
-    // re-read the reference samples from LDS (cheap, conflict-free) instead
-    // of letting the compiler keep all 36 in VGPRs across calls
-    asm volatile("" : "+v"(tb));
     float sum_src, sum_ss, sum_rs;
 #if ACMMP_FAST_RCP
     // hz is affine in the sample position, so its values over the patch lie
@@ -587,10 +541,10 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-    if (fast) ncc_sums<true>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
-    else ncc_sums<false>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
+    if (fast) ncc_sums<true>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    else ncc_sums<false>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #else
-    ncc_sums<false>(im, H, tile, tb, pp, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums<false>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #endif
     sum_src *= pp.inv_wsum;
     sum_ss *= pp.inv_wsum;
@@ -804,7 +758,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 template <int NS>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ WSlot wlds[kSamples * kThreads];
+    __shared__ float4 wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -895,7 +849,7 @@ template <int NS>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ WSlot wlds[kSamples * kThreads];
+    __shared__ float4 wlds[kSlots * kThreads];
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -1432,7 +1386,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ WSlot wlds[kSamples * kThreads];
+    __shared__ float4 wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1559,146 +1513,6 @@ __global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int 
     }
     out[(size_t)py * W + px] = total_val / normalizing_factor;
 }
-
-#if defined(ACMMP_DIAG_PROBE) && ACMMP_LDS_WR
-// ---- throughput probe (diagnostic builds only): one thread per (pixel,
-// candidate), the pixel's 36 (w, w*r) pairs precomputed and staged in LDS,
-// NCC against every source view; measures the split-kernel design.
-__global__ __launch_bounds__(256) void k_probe_prep(const KViews *__restrict__ kvp, int colour, float2 *wpair,
-                                                    float4 *stats, int P2) {
-    __shared__ float tile[kTileW * kTileH];
-    __shared__ WSlot wlds[kSamples * kThreads];
-    const KViews &kv = *kvp;
-    const BlockXY blk{(int)blockIdx.x, (int)blockIdx.y};
-    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
-    __syncthreads();
-    const LaneGeom g = lane_geom(colour, blk);
-    if (g.py >= kv.H || g.px >= kv.W) return;
-    PixPatch pp;
-    pp.wo = threadIdx.y * kBX + threadIdx.x;
-    pp.w = wlds + pp.wo;
-    pixel_patch(kv, tile, g.tb, g.s, pp);
-    const int my = g.py * kv.Wh + g.k;
-    for (int ii = 0; ii < kTaps; ++ii)
-        for (int jj = 0; jj < kTaps; ++jj) {
-            wpair[(size_t)widx(ii, jj) * P2 + my] = pp.w[widx(ii, jj) * kThreads];
-        }
-    stats[my] = make_float4(pp.mean, pp.var, pp.inv_wsum, 0.0f);
-}
-
-template <bool FAST, int PIPE>
-DEV void ncc_sums_lean(const SrcImage &im, const float *H, const float2 (*wl)[64], int lane, int px, int py,
-                       float &sum_src, float &sum_ss, float &sum_rs) {
-    sum_src = sum_ss = sum_rs = 0.0f;
-    ColFetch buf[PIPE ? 2 : 1];
-    if (PIPE) fetch_column<FAST>(im, H, (float)(px - 5), py, buf[0]);
-#pragma unroll
-    for (int ii = 0; ii < kTaps; ++ii) {
-        if (PIPE) {
-            if (ii + 1 < kTaps) fetch_column<FAST>(im, H, (float)(px - 5 + 2 * (ii + 1)), py, buf[(ii + 1) & 1]);
-        } else {
-            fetch_column<FAST>(im, H, (float)(px - 5 + 2 * ii), py, buf[0]);
-        }
-        const ColFetch &f = buf[PIPE ? (ii & 1) : 0];
-        float r_s = 0.0f;
-        f2v racc = f2v{0.0f, 0.0f};
-#pragma unroll
-        for (int jj = 0; jj < kTaps; ++jj) {
-            const float sv = bilinear_sample(f, jj);
-            const float2 w = wl[widx(ii, jj)][lane];
-            const float ws = w.x * sv;
-            r_s += ws;
-            racc = fma2(f2v{ws, w.y}, f2v{sv, sv}, racc);
-        }
-        sum_src += r_s;
-        sum_ss += racc.x;
-        sum_rs += racc.y;
-    }
-}
-
-template <int PIPE>
-__global__ __launch_bounds__(576) void k_probe(const KViews *__restrict__ kvp, KState st, int colour,
-                                                const float2 *__restrict__ wpair, const float4 *__restrict__ stats,
-                                                int P2, float *__restrict__ out) {
-    __shared__ float2 wl[kSamples][64];
-    const KViews &kv = *kvp;
-    const int lane = threadIdx.x, d = threadIdx.y;
-    const int k = blockIdx.x * 64 + lane, py = blockIdx.y;
-    const int Wh = kv.Wh;
-    for (int e = d * 64 + lane; e < kSamples * 64; e += 576) {
-        const int kk = blockIdx.x * 64 + (e & 63);
-        wl[e >> 6][e & 63] = kk < Wh ? wpair[(size_t)(e >> 6) * P2 + py * Wh + kk] : make_float2(0.f, 0.f);
-    }
-    __syncthreads();
-    const int s = (py + colour) & 1;
-    const int px = 2 * k + s;
-    if (px >= kv.W) return;
-    const int my = py * Wh + k;
-    const float4 ps = stats[my];
-    const int dx[9] = {0, 0, -3, 3, -1, 1, 0, 0, 0};
-    const int dy[9] = {-3, 3, 0, 0, 0, 0, -1, 1, 0};
-    const int nx = min(max(px + dx[d], 0), kv.W - 1), ny = min(max(py + dy[d], 0), kv.H - 1);
-    const float4 h = d == 8 ? st.plane[colour][my] : st.plane[colour ^ 1][ny * Wh + (nx >> 1)];
-    for (int v = 1; v <= kv.nsrc; ++v) {
-        float c = 2.0f;
-        if (ps.y >= 1e-5f) {
-            const SrcImage im = src_image(kv, v);
-            float H[9];
-            homography(kv, v, h, H);
-            const float2 pt = project(H, (float)px, (float)py);
-            if (!(pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f)) {
-                float sum_src, sum_ss, sum_rs;
-                if (PIPE == 2)
-                    ncc_sums_rows<true>(im, H, &wl[0][lane], 64, nullptr, 0, px, py, sum_src, sum_ss, sum_rs);
-                else ncc_sums_lean<true, PIPE>(im, H, wl, lane, px, py, sum_src, sum_ss, sum_rs);
-                sum_src *= ps.z;
-                sum_ss *= ps.z;
-                sum_rs *= ps.z;
-                const float var_src = sum_ss - sum_src * sum_src;
-                if (var_src >= 1e-5f) {
-                    const float covar = sum_rs - ps.x * sum_src;
-                    c = 1.0f - covar / dm_sqrt(ps.y * var_src);
-                    c = fminf(fmaxf(c, 0.0f), 2.0f);
-                }
-            }
-        }
-        out[(size_t)(d * 9 + v - 1) * P2 + my] = c;
-    }
-}
-
-static dim3 cs_grid(const KViews &kv, int colours);
-int probe_run(const KViews *d_kv, const KViews &h_kv, const KState &st, int variant, int reps, float *ms,
-              hipStream_t s) {
-    const int P2 = h_kv.H * h_kv.Wh;
-    float2 *wpair = nullptr;
-    float4 *stats = nullptr;
-    float *out = nullptr;
-    if (hipMalloc(&wpair, (size_t)kSamples * P2 * sizeof(float2)) != hipSuccess) return -3;
-    if (hipMalloc(&stats, (size_t)P2 * sizeof(float4)) != hipSuccess) return -3;
-    if (hipMalloc(&out, (size_t)81 * P2 * sizeof(float)) != hipSuccess) return -3;
-    k_probe_prep<<<cs_grid(h_kv, 1), dim3(kBX, kBY), 0, s>>>(d_kv, 0, wpair, stats, P2);
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    dim3 grid((h_kv.Wh + 63) / 64, h_kv.H), block(64, 9);
-    auto launch = [&]() {
-        if (variant == 0) k_probe<0><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-        else if (variant == 1) k_probe<1><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-        else k_probe<2><<<grid, block, 0, s>>>(d_kv, st, 0, wpair, stats, P2, out);
-    };
-    for (int w = 0; w < 2; ++w) launch();
-    hipEventRecord(a, s);
-    for (int r = 0; r < reps; ++r) launch();
-    hipEventRecord(b, s);
-    hipEventSynchronize(b);
-    hipEventElapsedTime(ms, a, b);
-    *ms /= reps;
-    hipFree(wpair);
-    hipFree(stats);
-    hipFree(out);
-    return 0;
-}
-#endif
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
