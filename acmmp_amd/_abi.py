@@ -245,6 +245,13 @@ def load_library(path: str | None = None) -> C.CDLL:
         raise RuntimeError(
             f"libacmmp_amd.so not found at {path}: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same
+    # soname as /opt/rocm's). Loaded first, it also serves this library; the
+    # other order leaves two runtimes and torch then finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -112,6 +113,14 @@ int kv_upload(acmmp_ctx *ctx) {
     kv.Wh = ctx->Wh;
     kv.sweep_rows = checkerboard_rows(ctx->H);
     kv.nsrc = ctx->n - 1;
+    // fp32 record indices are exact below 2^24 records (about 4090 x 4090);
+    // larger views (ETH3D high-res at native size) take the integer form.
+    // ACMMP_WIDE_INDEX=1 forces it (parity tests of that path at small sizes).
+    kv.wide = 0;
+    for (int i = 1; i < ctx->n; ++i)
+        if ((size_t)ctx->pad_pitch[i] * (ctx->cams[i].height + 2) >= (1u << 24)) kv.wide = 1;
+    if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
+        if (e[0] == '1') kv.wide = 1;
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737
@@ -256,10 +265,10 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         const int w = cams[i].width, h = cams[i].height;
         const int pp = (w + 3 + 15) / 16 * 16;  // float pairs per row (128-B rows)
         const size_t bytes = (size_t)pp * (h + 2) * 2 * sizeof(float);
-        // the gather kernels form record indices in fp32 (exact below 2^24):
-        // up to ~4090 x 4090 per view, above the reference's 3200 cap
-        if ((size_t)pp * (h + 2) >= (1u << 24))
-            return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^24-record gather limit", i, w, h);
+        // the gather kernels index records with a 24x24-bit multiply into a
+        // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
+        if ((size_t)pp * (h + 2) >= (1u << 31) || pp >= (1 << 24) || h + 2 >= (1 << 24))
+            return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^31-record gather limit", i, w, h);
         if (ctx->pad_bytes[i] < bytes) {
             HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
             ctx->pad_bytes[i] = bytes;

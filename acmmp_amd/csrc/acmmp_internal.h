@@ -48,6 +48,7 @@ struct KViews {
     int dw[ACMMP_MAX_IMAGES];
     int dh[ACMMP_MAX_IMAGES];
     int W, H, Wh, sweep_rows, nsrc;
+    int wide;                                 // some view has >= 2^24 padded records
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
 };

@@ -415,7 +415,7 @@ DEV float lerp_sample(u32x4 t, float ax, float ay) {
 // hypotheses are incoherent) and accumulated into per-column partial sums:
 // within a column the rows are still added in order jj = 0..5, columns are
 // summed at the end in order ii — the pinned order (src/ACMMP.cu:382-412).
-template <bool FAST>
+template <bool FAST, bool WIDE>
 DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int wstride, int px, int py,
                        float &sum_src, float &sum_ss, float &sum_rs) {
     f2v cx[kPairs], cy[kPairs], cz[kPairs];
@@ -468,11 +468,23 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
             const f2v fly = f2v{dm_floor(ys.x), dm_floor(ys.y)};
             ax[p] = xs - flx;
             ay[p] = ys - fly;
-            // record index (y0 + 1) * pitch + x0 + 1 = fma(y0, pitch, x0 + pitch + 1):
-            // integers below 2^24, so exact in fp32 (checked on the host)
-            const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
-            t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)(unsigned)idx.x, 0, 0, 0);
-            t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)(unsigned)idx.y, 0, 0, 0);
+            // record index (y0 + 1) * pitch + x0 + 1
+            unsigned ia, ib;
+            if (!WIDE) {
+                // = fma(y0, pitch, x0 + pitch + 1): integers below 2^24, so
+                // exact in fp32 (the engine selects WIDE otherwise)
+                const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
+                ia = (unsigned)idx.x;
+                ib = (unsigned)idx.y;
+            } else {
+                // views of 2^24 records or more: integer multiply-add (24-bit
+                // operands, 32-bit result)
+                const f2v q = flx + 1.0f, r = fly + 1.0f;
+                ia = __umul24((unsigned)r.x, (unsigned)im.pitch) + (unsigned)q.x;
+                ib = __umul24((unsigned)r.y, (unsigned)im.pitch) + (unsigned)q.y;
+            }
+            t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
+            t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
         }
 #pragma unroll
         for (int p = 0; p < kPairs; ++p) {
@@ -500,7 +512,7 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // returns the three weighted sums (ncc_sums_rows above).
-template <bool FAST>
+template <bool FAST, bool WIDE>
 DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
                   float &sum_ss, float &sum_rs) {
     // re-read weights from LDS each call rather than caching them in VGPRs
@@ -509,12 +521,13 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
     const float4 *wl = pp.w - pp.wo + wo;
-    ncc_sums_rows<FAST>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums_rows<FAST, WIDE>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
 // wave-uniform). Reference samples come from the LDS tile, source samples
 // through ncc_sums.
+template <bool WIDE>
 DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
                         int py, float4 h) {
     const float cost_max = 2.0f;
@@ -541,10 +554,10 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-    if (fast) ncc_sums<true>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-    else ncc_sums<false>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    if (fast) ncc_sums<true, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    else ncc_sums<false, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #else
-    ncc_sums<false>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums<false, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #endif
     sum_src *= pp.inv_wsum;
     sum_ss *= pp.inv_wsum;
@@ -560,7 +573,7 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
 }
 
 // ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
-template <int NS>
+template <int NS, bool WIDE>
 DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int px, int py,
                        float4 h, uint32_t &sel) {
     const int nsrc = kv.nsrc;
@@ -568,7 +581,7 @@ DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPat
     float cs[NS];
     int num_valid = 0;
     for (int i = 0; i < nsrc; ++i) {
-        const float c = bilateral_ncc(kv, tile, tb, pp, i + 1, px, py, h);
+        const float c = bilateral_ncc<WIDE>(kv, tile, tb, pp, i + 1, px, py, h);
         cv[i] = c;
         cs[i] = c;
         if (c < 2.0f) num_valid++;
@@ -755,7 +768,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
 // writes the colour-split "current" buffers. blockIdx.z = colour.
-template <int NS>
+template <int NS, bool WIDE>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ float4 wlds[kSlots * kThreads];
@@ -782,10 +795,10 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         const float depth = dm_rng_uniform(&rs) * (prm.depth_max - prm.depth_min) + prm.depth_min;
         plane = random_normal(c0, px, py, rs, depth);
         plane.w = distance_to_origin(c0, px, py, depth, plane);
-        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.seeded) {
         plane = st.seed[center];
-        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.planar_prior) {
         if (st.mask[center] > 0 && st.rm_cost[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -800,7 +813,7 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
             plane = st.rm_plane[center];
             plane.w = distance_to_origin(c0, px, py, plane.w, plane);
         }
-        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.upsample) {
         const float scale = (float)(1.0 * (double)prm.scaled_cols / (double)kv.W);
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -812,16 +825,16 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         float ucost;
         const float4 n_total = upscale_normal(kv, st, px, py, sigmad, sigmar, nn, o_y, o_x, refPix, ucost);
         const float4 prev = st.rm_plane[center];
-        st.pre_cost[center] = initial_cost<NS>(kv, tile, g.tb, pp, px, py, prev, sel);
+        st.pre_cost[center] = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, prev, sel);
         plane = to_cam(c0, n_total);
         plane.w = distance_to_origin(c0, px, py, prev.w, plane);
-        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else {
         float4 h = prm.hierarchy ? st.scaled[center] : st.rm_plane[center];
         h = to_cam(c0, h);
         h.w = distance_to_origin(c0, px, py, h.w, h);
         plane = h;
-        cost = initial_cost<NS>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
     }
     const int ci = py * kv.Wh + g.k;
     st.plane[colour][ci] = plane;
@@ -845,7 +858,7 @@ struct ViewCounts {
 // Neighbour state is read from the colour-split "current" buffers (the
 // half-sweep snapshot); own state lives in registers and is written to the
 // "next" buffer of this colour.
-template <int NS>
+template <int NS, bool WIDE>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
@@ -1068,7 +1081,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         float cv[8];
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
-            if ((flags >> d) & 1u) cv[d] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
+            if ((flags >> d) & 1u) cv[d] = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
             else cv[d] = (d == 0 && v == 0) ? 2.0f : 0.0f;
             cost_array[d][v] = cv[d];
         }
@@ -1176,7 +1189,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
-                const float c = bilateral_ncc(kv, tile, g.tb, pp, j + 1, px, py, h);
+                const float c = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, j + 1, px, py, h);
                 if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
                 else tc += wj * c;
             }
@@ -1382,7 +1395,7 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
 // T1 kernel: costs of a given plane per pixel against every source view.
 // T1 kernel: costs of a given plane per pixel against every source view
 // (same NCC code path as the sweep; blockIdx.z = colour).
-template <int NS>
+template <int NS, bool WIDE>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
@@ -1402,10 +1415,10 @@ __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ k
     const float4 h = planes[c];
     if (out)
         for (int v = 0; v < kv.nsrc; ++v)
-            out[(size_t)c * kv.nsrc + v] = bilateral_ncc(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
+            out[(size_t)c * kv.nsrc + v] = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
     if (out_init) {
         uint32_t sel = 0;
-        out_init[c] = initial_cost<NS>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
+        out_init[c] = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
         if (out_views) out_views[c] = sel;
     }
 }
@@ -1531,13 +1544,22 @@ static int ns_bucket(int nsrc) {
     return 32;
 }
 
-#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
+#define ACMMP_LAUNCH_NSW(KERNEL, W, GRID, BLOCK, STREAM, ...)                              \
     switch (ns_bucket(h_kv.nsrc)) {                                                         \
-        case 4: KERNEL<4><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                  \
-        case 9: KERNEL<9><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                  \
-        case 16: KERNEL<16><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
-        case 20: KERNEL<20><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
-        default: KERNEL<32><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;                \
+        case 4: KERNEL<4, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;               \
+        case 9: KERNEL<9, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;               \
+        case 16: KERNEL<16, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+        case 20: KERNEL<20, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+        default: KERNEL<32, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+    }
+
+// Source-view count -> array capacity; KViews::wide -> the integer record
+// index of views with 2^24 or more records.
+#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
+    if (h_kv.wide) {                                                                        \
+        ACMMP_LAUNCH_NSW(KERNEL, true, GRID, BLOCK, STREAM, __VA_ARGS__)                    \
+    } else {                                                                                \
+        ACMMP_LAUNCH_NSW(KERNEL, false, GRID, BLOCK, STREAM, __VA_ARGS__)                   \
     }
 
 static dim3 cs_grid(const KViews &kv, int colours) {

@@ -190,59 +190,88 @@ def render_numpy(setup: SceneSetup, i: int) -> View:
                 image=img, depth=z, normal=nrm.astype(np.float32).reshape(height, width, 3))
 
 
-def render_torch(setup: SceneSetup, i: int, device):
+def render_torch(setup: SceneSetup, i: int, device, with_depth: bool = False, rows_per_chunk: int = 256):
     """Same scene rendered with torch on `device` (fp64 geometry); returns the
-    (H, W) float32 image tensor on the device. Used by bench.py to build the
-    1600x1200 inputs directly in HBM; pixel values may differ from
-    render_numpy in rare rounding cases (not used for parity)."""
+    (H, W) float32 image tensor on the device (and, with_depth, the camera-z
+    depth map, 0 where no surface is hit). Used by bench.py and the GPU tests
+    to build inputs directly in HBM; pixel values may differ from
+    render_numpy in rare rounding cases (not used for parity).
+
+    Elementwise products only (no BLAS calls, whose algorithm choice at
+    24-Mpix shapes changed results between calls) and bounded chunks of rows,
+    so the output is deterministic and the temporaries stay small at ETH3D
+    sizes."""
     import torch
 
     R, t, C, _ = setup.poses[i]
     K, width, height = setup.K, setup.width, setup.height
     dt = torch.float64
-    Rt = torch.tensor(R, dtype=dt, device=device)
-    Ct = torch.tensor(C, dtype=dt, device=device)
-    ys, xs = torch.meshgrid(torch.arange(height, dtype=dt, device=device),
-                            torch.arange(width, dtype=dt, device=device), indexing="ij")
-    dc = torch.stack([(xs - K[0, 2]) / K[0, 0], (ys - K[1, 2]) / K[1, 1], torch.ones_like(xs)], -1).reshape(-1, 3)
-    Dw = dc @ Rt
-    D = Dw / torch.linalg.norm(Dw, dim=1, keepdim=True)
-    n = D.shape[0]
-    best = torch.full((n,), float("inf"), dtype=dt, device=device)
-    pn = np.array([0.25, -0.15, 1.0])
-    pn = torch.tensor(pn / np.linalg.norm(pn), dtype=dt, device=device)
-    s = (-160.0 - Ct @ pn) / (D @ pn)
-    ok = (s > 1e-3) & torch.isfinite(s) & (s < best)
-    best = torch.where(ok, s, best)
-    cs = torch.tensor([-20.0, 10.0, 0.0], dtype=dt, device=device)
-    oc = Ct - cs
-    b = D @ oc
-    disc = b * b - (oc @ oc - 85.0 * 85.0)
-    s = -b - torch.sqrt(torch.clamp(disc, min=0.0))
-    ok = (disc > 0) & (s > 1e-3) & (s < best)
-    best = torch.where(ok, s, best)
-    bmin = torch.tensor([60.0, -40.0, -60.0], dtype=dt, device=device)
-    bmax = torch.tensor([150.0, 50.0, 20.0], dtype=dt, device=device)
-    t1 = (bmin - Ct) / D
-    t2 = (bmax - Ct) / D
-    tn = torch.minimum(t1, t2).max(dim=1).values
-    tf = torch.maximum(t1, t2).min(dim=1).values
-    ok = (tn <= tf) & (tn > 1e-3) & (tn < best)
-    best = torch.where(ok, tn, best)
-    hit = torch.isfinite(best)
-    X = Ct + torch.where(hit, best, torch.zeros_like(best))[:, None] * D
     tex = setup.texture
-    f = torch.tensor(tex.f.T, dtype=dt, device=device)
-    sv = torch.sin(X @ f + torch.tensor(tex.phase, dtype=dt, device=device)) @ torch.tensor(tex.amp, dtype=dt,
-                                                                                          device=device)
-    sv = sv / float(np.sqrt(0.5 * np.sum(tex.amp ** 2)))
-    val = 127.5 + 60.0 * torch.tanh(0.9 * sv)
-    low = torch.sin(X @ torch.tensor(tex.f2.T, dtype=dt, device=device) +
-                    torch.tensor(tex.p2, dtype=dt, device=device)).sum(dim=1) / float(np.sqrt(3.0))
-    val = torch.where(low > 1.28, torch.full_like(val, 128.0), val)
-    val = torch.where(hit, val, torch.full_like(val, 40.0))
-    img = torch.clamp(torch.round(val), 0, 255).to(torch.float32).reshape(height, width).contiguous()
-    return img
+    pn = np.array([0.25, -0.15, 1.0])
+    pn = pn / np.linalg.norm(pn)
+    cs = np.array([-20.0, 10.0, 0.0])
+    bmin, bmax = np.array([60.0, -40.0, -60.0]), np.array([150.0, 50.0, 20.0])
+    Cpn = float(C @ pn)
+    oc = C - cs
+    occ = float(oc @ oc)
+
+    def lin(cols, coef):  # sum_k cols[k] * coef[k] (coef: host fp64 scalars or rows)
+        out = cols[0] * coef[0]
+        for k in range(1, len(cols)):
+            out = out + cols[k] * coef[k]
+        return out
+
+    img = torch.empty((height, width), dtype=torch.float32, device=device)
+    dep = torch.empty((height, width), dtype=torch.float32, device=device) if with_depth else None
+    xs1 = torch.arange(width, dtype=dt, device=device)
+    f = [torch.tensor(tex.f[:, k], dtype=dt, device=device) for k in range(3)]
+    f2 = [torch.tensor(tex.f2[:, k], dtype=dt, device=device) for k in range(3)]
+    phase = torch.tensor(tex.phase, dtype=dt, device=device)
+    p2 = torch.tensor(tex.p2, dtype=dt, device=device)
+    amp = torch.tensor(tex.amp, dtype=dt, device=device)
+    amp_norm = float(np.sqrt(0.5 * np.sum(tex.amp ** 2)))
+    for r0 in range(0, height, rows_per_chunk):
+        r1 = min(height, r0 + rows_per_chunk)
+        ys, xs = torch.meshgrid(torch.arange(r0, r1, dtype=dt, device=device), xs1, indexing="ij")
+        dc = [((xs - K[0, 2]) / K[0, 0]).reshape(-1), ((ys - K[1, 2]) / K[1, 1]).reshape(-1)]
+        dc.append(torch.ones_like(dc[0]))
+        Dw = [lin(dc, R[:, j]) for j in range(3)]  # R^T d
+        nrm = torch.sqrt(Dw[0] * Dw[0] + Dw[1] * Dw[1] + Dw[2] * Dw[2])
+        D = [d / nrm for d in Dw]
+        best = torch.full_like(nrm, float("inf"))
+        # background plane
+        s = (-160.0 - Cpn) / lin(D, pn)
+        ok = (s > 1e-3) & torch.isfinite(s) & (s < best)
+        best = torch.where(ok, s, best)
+        # sphere
+        b = lin(D, oc)
+        disc = b * b - (occ - 85.0 * 85.0)
+        s = -b - torch.sqrt(torch.clamp(disc, min=0.0))
+        ok = (disc > 0) & (s > 1e-3) & (s < best)
+        best = torch.where(ok, s, best)
+        # axis-aligned box
+        t1 = [(bmin[k] - C[k]) / D[k] for k in range(3)]
+        t2 = [(bmax[k] - C[k]) / D[k] for k in range(3)]
+        tn = torch.maximum(torch.maximum(torch.minimum(t1[0], t2[0]), torch.minimum(t1[1], t2[1])),
+                           torch.minimum(t1[2], t2[2]))
+        tf = torch.minimum(torch.minimum(torch.maximum(t1[0], t2[0]), torch.maximum(t1[1], t2[1])),
+                           torch.maximum(t1[2], t2[2]))
+        ok = (tn <= tf) & (tn > 1e-3) & (tn < best)
+        best = torch.where(ok, tn, best)
+        hit = torch.isfinite(best)
+        sh = torch.where(hit, best, torch.zeros_like(best))
+        X = [C[k] + sh * D[k] for k in range(3)]
+        arg = lin([x[:, None] for x in X], f) + phase
+        sv = (torch.sin(arg) * amp).sum(dim=1) / amp_norm
+        val = 127.5 + 60.0 * torch.tanh(0.9 * sv)
+        low = torch.sin(lin([x[:, None] for x in X], f2) + p2).sum(dim=1) / float(np.sqrt(3.0))
+        val = torch.where(low > 1.28, torch.full_like(val, 128.0), val)
+        val = torch.where(hit, val, torch.full_like(val, 40.0))
+        img[r0:r1] = torch.clamp(torch.round(val), 0, 255).to(torch.float32).reshape(r1 - r0, width)
+        if with_depth:
+            dep[r0:r1] = torch.where(hit, best / torch.sqrt(dc[0] * dc[0] + dc[1] * dc[1] + 1.0),
+                                     torch.zeros_like(best)).to(torch.float32).reshape(r1 - r0, width)
+    return (img, dep) if with_depth else img
 
 
 def make_scene(num_views: int = 10, width: int = 1600, height: int = 1200, seed: int = 0x5EED,
