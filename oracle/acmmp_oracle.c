@@ -36,7 +36,8 @@
  * Parity status: the reference cannot be built or run here (CUDA/cuRAND/OpenCV
  * absent) and ships no tests or fixtures for this path, so this
  * restatement is "parity unpinned" against reference outputs; it is pinned by
- * analytic known-answer tests (tests/test_oracle_kat.py) and by the
+ * analytic known-answer tests (tests/test_oracle_kat.py: analytic answers, an fp64 restatement
+ * of the NCC/homography/geometric cost, bit-exact init-cost aggregation) and by the
  * reference converter's cams/pair fixtures for the I/O formats.
  */
 #include <float.h>
