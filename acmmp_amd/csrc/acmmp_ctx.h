@@ -34,6 +34,8 @@ struct acmmp_ctx {
     std::vector<float *> pad;          // padded source images (KViews::pad), owned
     std::vector<size_t> pad_bytes;
     std::vector<int> pad_pitch;
+    bool pad_u8 = false;               // pad[] hold u8 quads (KViews::u8)
+    uint32_t *d_not_u8 = nullptr;      // device flag of the u8 check
     std::vector<int> dep_pitch, dep_w, dep_h;
     bool have_depths = false;
 

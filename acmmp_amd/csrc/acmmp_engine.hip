@@ -121,6 +121,7 @@ int kv_upload(acmmp_ctx *ctx) {
         if ((size_t)ctx->pad_pitch[i] * (ctx->cams[i].height + 2) >= (1u << 24)) kv.wide = 1;
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
+    kv.u8 = ctx->pad_u8 ? 1 : 0;
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737
@@ -261,20 +262,49 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         ctx->pad_bytes.resize(num_images, 0);
         ctx->pad_pitch.resize(num_images, 0);
     }
-    for (int i = 0; i < num_images; ++i) {
-        const int w = cams[i].width, h = cams[i].height;
-        const int pp = (w + 3 + 15) / 16 * 16;  // float pairs per row (128-B rows)
-        const size_t bytes = (size_t)pp * (h + 2) * 2 * sizeof(float);
-        // the gather kernels index records with a 24x24-bit multiply into a
-        // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
-        if ((size_t)pp * (h + 2) >= (1u << 31) || pp >= (1 << 24) || h + 2 >= (1 << 24))
-            return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^31-record gather limit", i, w, h);
-        if (ctx->pad_bytes[i] < bytes) {
-            HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
-            ctx->pad_bytes[i] = bytes;
+    // First the u8 quad form (4 B per footprint): valid when every view is
+    // integer-valued in [0, 255], which one device flag reports (one stream
+    // sync). Otherwise the fp32 row-paired form (16 B per footprint) is built
+    // over it. ACMMP_TEXEL_F32=1 forces the fp32 form (parity tests of both).
+    bool force_f32 = false;
+    if (const char *e = std::getenv("ACMMP_TEXEL_F32")) force_f32 = e[0] == '1';
+    if (!ctx->d_not_u8) HIP_TRY(ctx, dalloc(ctx->d_not_u8, 1));
+    for (int pass = force_f32 ? 1 : 0; pass < 2; ++pass) {
+        if (pass == 0) HIP_TRY(ctx, hipMemsetAsync(ctx->d_not_u8, 0, sizeof(uint32_t), ctx->stream));
+        for (int i = 0; i < num_images; ++i) {
+            const int w = cams[i].width, h = cams[i].height;
+            // records per row: u8 quads (W + 2, 128-B rows) or fp32 row pairs
+            // (W + 3, 128-B rows); the f32 form is the larger allocation
+            const int pq = (w + 2 + 31) / 32 * 32, pf = (w + 3 + 15) / 16 * 16;
+            const int pp = pass == 0 ? pq : pf;
+            const size_t bytes = (size_t)pf * (h + 2) * 2 * sizeof(float);
+            // the gather kernels index records with a 24x24-bit multiply into a
+            // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
+            if ((size_t)pf * (h + 2) >= (1u << 31) || pf >= (1 << 24) || h + 2 >= (1 << 24))
+                return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^31-record gather limit", i,
+                               w, h);
+            if (ctx->pad_bytes[i] < bytes) {
+                dfree(ctx->pad[i]);
+                HIP_TRY(ctx, dalloc(ctx->pad[i], bytes / sizeof(float)));
+                ctx->pad_bytes[i] = bytes;
+            }
+            ctx->pad_pitch[i] = pp;
+            if (pass == 0)
+                HIP_TRY(ctx, launch_pad_quad(ctx->img[i], ctx->img_pitch[i], w, h,
+                                             reinterpret_cast<uint32_t *>(ctx->pad[i]), pp, ctx->d_not_u8,
+                                             ctx->stream));
+            else
+                HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
         }
-        ctx->pad_pitch[i] = pp;
-        HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
+        if (pass == 0) {
+            uint32_t not_u8 = 1;
+            HIP_TRY(ctx, hipMemcpyAsync(&not_u8, ctx->d_not_u8, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            ctx->pad_u8 = not_u8 == 0;
+            if (ctx->pad_u8) break;
+        } else {
+            ctx->pad_u8 = false;
+        }
     }
     if (resize || !ctx->d_rm_plane) {
         free_state(ctx);
@@ -345,6 +375,11 @@ int acmmp_device_count(void) {
     return n;
 }
 
+int acmmp_get_texel_bits(const acmmp_ctx *ctx) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    return ctx->pad_u8 ? 8 : 32;
+}
+
 const char *acmmp_version(void) {
     return "acmmp_amd 0.1 gfx950 (-O3 -ffp-contract=off, IEEE div/sqrt, pinned detmath)";
 }
@@ -374,6 +409,7 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     free_images(ctx);
     free_state(ctx);
     for (auto &p : ctx->pad) dfree(p);
+    dfree(ctx->d_not_u8);
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
         dfree(ctx->d_kv_ring[k]);
         if (ctx->h_kv_ring[k]) (void)hipHostFree(ctx->h_kv_ring[k]);

@@ -36,19 +36,23 @@ struct KViews {
     ViewRel rel[ACMMP_MAX_IMAGES];            // rel[v] for source v (1-based), rel[0] unused
     const float *img[ACMMP_MAX_IMAGES];       // pitched images
     int ipitch[ACMMP_MAX_IMAGES];             // in floats
-    // Source images with clamp-to-edge baked in, row-paired: element (r, c)
-    // (r < H + 2, c < W + 3) is the float pair (texel(clamp(c-1), clamp(r-1)),
-    // texel(clamp(c-1), clamp(r))), so the 2x2 bilinear footprint of a
-    // coordinate clamped to [-1, W] x [-1, H] is ONE 16-byte load, without
-    // integer clamps or selects.
+    // Source images with clamp-to-edge baked in, so the 2x2 bilinear
+    // footprint of a coordinate clamped to [-1, W] x [-1, H] is ONE load at
+    // record (y0 + 1, x0 + 1), without integer clamps or selects. Either
+    //  * u8 quads (u8 = 1): record (r, c), r < H + 2, c < W + 2, packs the
+    //    bytes of texels (c-1, r-1), (c-1, r), (c, r-1), (c, r) (clamped):
+    //    4 B per footprint, when every view is integer-valued in [0, 255];
+    //  * fp32 row pairs: record (r, c), c < W + 3, is the float pair
+    //    (texel(c-1, r-1), texel(c-1, r)); a footprint is two records, 16 B.
     const float *pad[ACMMP_MAX_IMAGES];
-    int ppitch[ACMMP_MAX_IMAGES];             // in float pairs
+    int ppitch[ACMMP_MAX_IMAGES];             // in records
     const float *dep[ACMMP_MAX_IMAGES];       // pitched depth maps (geom consistency)
     int dpitch[ACMMP_MAX_IMAGES];
     int dw[ACMMP_MAX_IMAGES];
     int dh[ACMMP_MAX_IMAGES];
     int W, H, Wh, sweep_rows, nsrc;
     int wide;                                 // some view has >= 2^24 padded records
+    int u8;                                   // pad[] hold u8 texel quads (every view integer-valued 0..255)
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
 };
@@ -85,6 +89,10 @@ hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4
 
 hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch,
                             hipStream_t stream);
+// u8 texel-quad copy of one view; sets *not_u8 = 1 if a texel is not an
+// integer in [0, 255] (the copy is then unusable and the fp32 form is built).
+hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch,
+                           uint32_t *not_u8, hipStream_t stream);
 int diag_read_cycles(unsigned long long *out8);
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);

@@ -268,23 +268,36 @@ DEV float2 project(const float *H, float x, float y) {
     return make_float2(px * inv, py * inv);
 }
 
+// Texel modes of the gather kernels (template parameter TX):
+//   bit 0 (kTxWide): record index by integer multiply-add (views of 2^24+
+//          records), else exactly in fp32;
+//   bit 1 (kTxU8):   the padded source views hold u8 texel quads (every view
+//          of the problem is integer-valued in [0, 255], which 8-bit JPEG
+//          input at native size is): one 4-byte record per bilinear
+//          footprint instead of 16 bytes; v_cvt_f32_ubyte* restores the exact
+//          fp32 texel values, so the arithmetic is unchanged.
+constexpr int kTxWide = 1, kTxU8 = 2;
+
 // Source-image sampler: one buffer resource (SRD) per view over the padded
 // copy (KViews::pad), built from wave-uniform values (the view index is a
-// uniform loop counter) so the loads are `buffer_load_dwordx2 ... offen` with
-// 32-bit offsets and the row stride in the SGPR soffset.
+// uniform loop counter) so the loads are index-addressed (`idxen`) buffer
+// loads with the record stride in the descriptor.
 struct SrcImage {
     __amdgpu_buffer_rsrc_t rsrc;
     int pitch, W, H;
     float fpitch, fp1;  // pitch and pitch + 1 as floats (exact: < 2^24)
 };
 
+template <int TX>
 DEV SrcImage src_image(const KViews &kv, int v) {
     SrcImage s;
     s.pitch = kv.ppitch[v];
     s.W = kv.cam[v].width;
     s.H = kv.cam[v].height;
-    // structured view: 8-byte records (one row pair), indexed loads (idxen)
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)8, s.pitch * (s.H + 2), 0x00020000);
+    // structured view, indexed loads (idxen): 8-byte records (one fp32 row
+    // pair) or 4-byte records (one u8 2x2 quad)
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)kv.pad[v], (short)((TX & kTxU8) ? 4 : 8), s.pitch * (s.H + 2),
+                                               0x00020000);
     s.fp1 = (float)(s.pitch + 1);
     s.fpitch = (float)s.pitch;
     return s;
@@ -330,17 +343,18 @@ constexpr int kSlots = kPairs * kTaps;
 DEV int wslot(int p, int jj) { return jj * kPairs + p; }
 
 struct PixPatch {
-    float4 *w;       // LDS: slot k of this lane at [k * kThreads]
+    float2 *w;       // LDS: slot k of this lane at [k * kThreads]
+    const float *rt; // LDS: this lane's first reference sample in the tile (tile + tb)
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
     float var;       // var_ref
     float inv_wsum;  // inv_bilateral_weight_sum
 };
 
-// 18 float4 rows of 256 lanes: 72 KB + the 3.9 KB tile per 256-thread block
-// (2 blocks = the 8 waves of a CU at this kernel's occupancy). A wave's read
-// of one slot is a conflict-free ds_read_b128 and costs no VGPRs between
-// NCC calls.
+// 18 float2 rows of 256 lanes: 36 KB + the 3.9 KB tile per 256-thread block,
+// so four blocks (16 waves) fit a CU's 160 KB of LDS. A wave's read of one
+// slot is a conflict-free ds_read_b64 and costs no VGPRs between NCC calls;
+// the matching reference pair comes from the tile (ds_read2_b32).
 constexpr int kThreads = kBX * kBY;
 
 DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, float sc) {
@@ -367,7 +381,6 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_w += w;
             float *slot = reinterpret_cast<float *>(&pp.w[wslot(ii >> 1, jj) * kThreads]);
             slot[ii & 1] = w;
-            slot[2 + (ii & 1)] = wr;
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -388,6 +401,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // (address = base + vindex * stride + voffset); clang has no builtin for it.
 __device__ u32x4 amdgcn_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                 int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+__device__ unsigned amdgcn_struct_buffer_load_b32(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                                                  int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
+
+// u8 quad (t00, t01, t10, t11) -> the fp32 texels, exactly (v_cvt_f32_ubyte0..3)
+DEV u32x4 unpack_quad(unsigned q) {
+    return u32x4{__float_as_uint((float)(q & 0xffu)), __float_as_uint((float)((q >> 8) & 0xffu)),
+                 __float_as_uint((float)((q >> 16) & 0xffu)), __float_as_uint((float)(q >> 24))};
+}
 
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 DEV f2v splat(float v) { return f2v{v, v}; }
@@ -415,9 +436,9 @@ DEV float lerp_sample(u32x4 t, float ax, float ay) {
 // hypotheses are incoherent) and accumulated into per-column partial sums:
 // within a column the rows are still added in order jj = 0..5, columns are
 // summed at the end in order ii — the pinned order (src/ACMMP.cu:382-412).
-template <bool FAST, bool WIDE>
-DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int wstride, int px, int py,
-                       float &sum_src, float &sum_ss, float &sum_rs) {
+template <bool FAST, int TX>
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, const float *rt, int wstride, int px,
+                       int py, float &sum_src, float &sum_ss, float &sum_rs) {
     f2v cx[kPairs], cy[kPairs], cz[kPairs];
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
@@ -426,6 +447,7 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
         cy[p] = fma2(splat(H[3]), x, splat(H[5]));
         cz[p] = fma2(splat(H[6]), x, splat(H[8]));
     }
+    constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0;
     f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
@@ -436,6 +458,7 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
     for (int jj = 0; jj < kTaps; ++jj) {
         const f2v y = splat((float)(py - 5 + 2 * jj));
         u32x4 t[kTaps];
+        unsigned q[kTaps];
         f2v ax[kPairs], ay[kPairs];
 #pragma unroll
         for (int p = 0; p < kPairs; ++p) {
@@ -483,17 +506,41 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
                 ia = __umul24((unsigned)r.x, (unsigned)im.pitch) + (unsigned)q.x;
                 ib = __umul24((unsigned)r.y, (unsigned)im.pitch) + (unsigned)q.y;
             }
-            t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
-            t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
+            if (U8) {
+#ifdef ACMMP_DIAG_NOGATHER  // timing experiment only: no memory access
+                q[2 * p] = ia * 0x01010101u;
+                q[2 * p + 1] = ib * 0x01010101u;
+#else
+                q[2 * p] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ia, 0, 0, 0);
+                q[2 * p + 1] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ib, 0, 0, 0);
+#endif
+            } else {
+                t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
+                t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int p = 0; p < kPairs; ++p) {
+            if (U8) {
+                t[2 * p] = unpack_quad(q[2 * p]);
+                t[2 * p + 1] = unpack_quad(q[2 * p + 1]);
+            }
             const f2v sv = f2v{lerp_sample(t[2 * p], ax[p].x, ay[p].x), lerp_sample(t[2 * p + 1], ax[p].y, ay[p].y)};
-            const float4 w = wl[wslot(p, jj) * wstride];
-            const f2v ws = f2v{w.x, w.y} * sv;
+            // w from the weight slots, ref from the tile: w * ref is the same
+            // IEEE product pixel_patch formed, so re-forming it is exact
+#ifdef ACMMP_DIAG_NOLDS  // timing experiment only: no LDS reads in the sample loop
+            const float2 w = make_float2(ax[p].x, ay[p].y);
+            const float rr[2] = {ax[p].y, ay[p].x};
+#else
+            const float2 w = wl[wslot(p, jj) * wstride];
+            const float *rr = rt + 2 * kTileW * jj + 2 * p;
+#endif
+            const f2v wv = f2v{w.x, w.y};
+            const f2v wr = wv * f2v{rr[0], rr[1]};
+            const f2v ws = wv * sv;
             acc_s[p] += ws;
             acc_ss[p] = fma2(ws, sv, acc_ss[p]);
-            acc_rs[p] = fma2(f2v{w.z, w.w}, sv, acc_rs[p]);
+            acc_rs[p] = fma2(wr, sv, acc_rs[p]);
         }
     }
     sum_src = 0.0f;
@@ -512,7 +559,7 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float4 *wl, int
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // returns the three weighted sums (ncc_sums_rows above).
-template <bool FAST, bool WIDE>
+template <bool FAST, int TX>
 DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
                   float &sum_ss, float &sum_rs) {
     // re-read weights from LDS each call rather than caching them in VGPRs
@@ -520,14 +567,14 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     // stays visible and the reads are ds_read, not flat)
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
-    const float4 *wl = pp.w - pp.wo + wo;
-    ncc_sums_rows<FAST, WIDE>(im, H, wl, kThreads, px, py, sum_src, sum_ss, sum_rs);
+    const float2 *wl = pp.w - pp.wo + wo;
+    ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
 // wave-uniform). Reference samples come from the LDS tile, source samples
 // through ncc_sums.
-template <bool WIDE>
+template <int TX>
 DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
                         int py, float4 h) {
     const float cost_max = 2.0f;
@@ -535,7 +582,7 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     // var_ref is invariant: when it is below kMinVar (or the centre maps
     // outside the source) every call returns cost_max.
     if (pp.var < kMinVar) return cost_max;
-    const SrcImage im = src_image(kv, v);
+    const SrcImage im = src_image<TX>(kv, v);
     float H[9];
     homography(kv, v, h, H);
     const float2 pt = project(H, (float)px, (float)py);
@@ -554,10 +601,10 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-    if (fast) ncc_sums<true, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-    else ncc_sums<false, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #else
-    ncc_sums<false, WIDE>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #endif
     sum_src *= pp.inv_wsum;
     sum_ss *= pp.inv_wsum;
@@ -573,7 +620,7 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
 }
 
 // ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
-template <int NS, bool WIDE>
+template <int NS, int TX>
 DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int px, int py,
                        float4 h, uint32_t &sel) {
     const int nsrc = kv.nsrc;
@@ -581,7 +628,7 @@ DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPat
     float cs[NS];
     int num_valid = 0;
     for (int i = 0; i < nsrc; ++i) {
-        const float c = bilateral_ncc<WIDE>(kv, tile, tb, pp, i + 1, px, py, h);
+        const float c = bilateral_ncc<TX>(kv, tile, tb, pp, i + 1, px, py, h);
         cv[i] = c;
         cs[i] = c;
         if (c < 2.0f) num_valid++;
@@ -715,7 +762,7 @@ DEV float4 upscale_normal(const KViews &kv, const KState &st, int px, int py, fl
 // ACMMP_DIAG_STAMPS builds only (never the product library): per-phase
 // s_memtime cycle sums of the sweep kernel, accumulated by lane 0 of each wave.
 #ifdef ACMMP_DIAG_STAMPS
-__device__ unsigned long long g_diag_cycles[8];
+__device__ unsigned long long g_diag_cycles[16];
 #define DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define DIAG_ADD(slot, a, b) \
     do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[slot], (b) - (a)); } while (0)
@@ -768,10 +815,10 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
 // writes the colour-split "current" buffers. blockIdx.z = colour.
-template <int NS, bool WIDE>
+template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float4 wlds[kSlots * kThreads];
+    __shared__ float2 wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -787,6 +834,7 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
     PixPatch pp;
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
+    pp.rt = tile + g.tb;
     pixel_patch(kv, tile, g.tb, g.s, pp);
     float4 plane;
     float cost;
@@ -795,10 +843,10 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         const float depth = dm_rng_uniform(&rs) * (prm.depth_max - prm.depth_min) + prm.depth_min;
         plane = random_normal(c0, px, py, rs, depth);
         plane.w = distance_to_origin(c0, px, py, depth, plane);
-        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.seeded) {
         plane = st.seed[center];
-        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.planar_prior) {
         if (st.mask[center] > 0 && st.rm_cost[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -813,7 +861,7 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
             plane = st.rm_plane[center];
             plane.w = distance_to_origin(c0, px, py, plane.w, plane);
         }
-        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else if (prm.upsample) {
         const float scale = (float)(1.0 * (double)prm.scaled_cols / (double)kv.W);
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -825,16 +873,16 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
         float ucost;
         const float4 n_total = upscale_normal(kv, st, px, py, sigmad, sigmar, nn, o_y, o_x, refPix, ucost);
         const float4 prev = st.rm_plane[center];
-        st.pre_cost[center] = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, prev, sel);
+        st.pre_cost[center] = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, prev, sel);
         plane = to_cam(c0, n_total);
         plane.w = distance_to_origin(c0, px, py, prev.w, plane);
-        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, plane, sel);
     } else {
         float4 h = prm.hierarchy ? st.scaled[center] : st.rm_plane[center];
         h = to_cam(c0, h);
         h.w = distance_to_origin(c0, px, py, h.w, h);
         plane = h;
-        cost = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, px, py, plane, sel);
+        cost = initial_cost<NS, TX>(kv, tile, g.tb, pp, px, py, plane, sel);
     }
     const int ci = py * kv.Wh + g.k;
     st.plane[colour][ci] = plane;
@@ -858,11 +906,11 @@ struct ViewCounts {
 // Neighbour state is read from the colour-split "current" buffers (the
 // half-sweep snapshot); own state lives in registers and is written to the
 // "next" buffer of this colour.
-template <int NS, bool WIDE>
+template <int NS, int TX>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float4 wlds[kSlots * kThreads];
+    __shared__ float2 wlds[kSlots * kThreads];
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -1030,11 +1078,19 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     }
 #undef CS
     auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
+    // wave-uniform d: select chain instead of a dynamically indexed (scratch) array
+    auto cand_dyn = [&](int d) -> float4 {
+        int ci = cidx[0];
+#pragma unroll
+        for (int e = 1; e < 8; ++e) ci = (d == e) ? cidx[e] : ci;
+        return (((same >> d) & 1u) ? plane_same : plane_opp)[ci];
+    };
 
     DIAG_T(t_search);
     PixPatch pp;
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
+    pp.rt = tile + g.tb;
     pixel_patch(kv, tile, g.tb, g.s, pp);
     DIAG_T(t_patch);
 
@@ -1075,31 +1131,37 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         atomicAdd(&g_diag_cycles[5], n);
         atomicAdd(&g_diag_cycles[6], dup);
         atomicAdd(&g_diag_cycles[7], cur);
+        // wave-level: max unique candidates over the wave (slot 12), lanes' sum
+        // (11), waves (10)
+        const int uniq = (int)(n - dup);
+        atomicAdd(&g_diag_cycles[11], (unsigned long long)uniq);
+        unsigned long long wmax = 0;
+        for (int u = 1; u <= 8; ++u) wmax += __ballot(uniq >= u) != 0;
+        if ((threadIdx.x & 63) == 0) { atomicAdd(&g_diag_cycles[12], wmax); atomicAdd(&g_diag_cycles[10], 1ull); }
     }
 #endif
     for (int v = 0; v < nsrc; ++v) {
-        float cv[8];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            if ((flags >> d) & 1u) cv[d] = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
-            else cv[d] = (d == 0 && v == 0) ? 2.0f : 0.0f;
-            cost_array[d][v] = cv[d];
-        }
-        float vsp = 0.0f;
-        for (int n = 0; n < 4; ++n)
-            if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> v) & 1u) ? 0.9f : 0.1f;
+        // one NCC call site: the candidate loop stays rolled (d is wave-uniform,
+        // the candidate's index is picked by selects), and the sampling
+        // statistics of :1013-1024 are accumulated in the same j = 0..7 order
         float count = 0;
         int count_false = 0;
         float tmpw = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const float c = cv[j];
+#pragma unroll 1
+        for (int d = 0; d < 8; ++d) {
+            float c;
+            if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand_dyn(d));
+            else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
+            cost_array[d][v] = c;
             if (c < cost_threshold) {
                 tmpw += dm_expf(c * c / (-0.18f));
                 count++;
             }
             if (c > 1.2f) count_false++;
         }
+        float vsp = 0.0f;
+        for (int n = 0; n < 4; ++n)
+            if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> v) & 1u) ? 0.9f : 0.1f;
         float pr = 0.0f;
         if (count > 2 && count_false < 3) pr = tmpw / count;
         else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
@@ -1133,6 +1195,15 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         if (c > 0) { temp_sv |= (1u << i); weight_norm += (float)c; }
     }
 
+#ifdef ACMMP_DIAG_STAMPS
+    {  // refinement divergence: views with a sampled weight per lane (9) vs the
+       // union over the wave (8)
+        unsigned long long uni = 0;
+        for (int v = 0; v < nsrc; ++v) uni += __ballot(vw.get(v) > 0) != 0;
+        atomicAdd(&g_diag_cycles[9], (unsigned long long)__builtin_popcount(temp_sv));
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[8], uni);
+    }
+#endif
     float final_costs[8];
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
@@ -1189,7 +1260,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
-                const float c = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, j + 1, px, py, h);
+                const float c = bilateral_ncc<TX>(kv, tile, g.tb, pp, j + 1, px, py, h);
                 if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
                 else tc += wj * c;
             }
@@ -1395,11 +1466,11 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
 // T1 kernel: costs of a given plane per pixel against every source view.
 // T1 kernel: costs of a given plane per pixel against every source view
 // (same NCC code path as the sweep; blockIdx.z = colour).
-template <int NS, bool WIDE>
+template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float4 wlds[kSlots * kThreads];
+    __shared__ float2 wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1411,14 +1482,15 @@ __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ k
     PixPatch pp;
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
+    pp.rt = tile + g.tb;
     pixel_patch(kv, tile, g.tb, g.s, pp);
     const float4 h = planes[c];
     if (out)
         for (int v = 0; v < kv.nsrc; ++v)
-            out[(size_t)c * kv.nsrc + v] = bilateral_ncc<WIDE>(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
+            out[(size_t)c * kv.nsrc + v] = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
     if (out_init) {
         uint32_t sel = 0;
-        out_init[c] = initial_cost<NS, WIDE>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
+        out_init[c] = initial_cost<NS, TX>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
         if (out_views) out_views[c] = sel;
     }
 }
@@ -1453,11 +1525,39 @@ hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *d
     return hipGetLastError();
 }
 
+// u8 quad layout: element (r, c), r < H + 2, c < W + 2, packs the texels
+// (clamp(c-1), clamp(r-1)), (clamp(c-1), clamp(r)), (clamp(c), clamp(r-1)),
+// (clamp(c), clamp(r)) as bytes 0..3, so the record at (y0 + 1, x0 + 1) is
+// the whole bilinear footprint of (x0, y0) (same record index as the fp32
+// row-paired copy). Texel (clamp(c-1), clamp(r-1)) ranges over every texel,
+// so checking it checks the view: -0.0f, NaN and non-integers are not u8.
+__global__ __launch_bounds__(256) void k_pad_quad(const float *__restrict__ src, int spitch, int W, int H,
+                                                  uint32_t *__restrict__ dst, int dpitch, uint32_t *not_u8) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int r = blockIdx.y * 4 + threadIdx.y;
+    if (c >= W + 2 || r >= H + 2) return;
+    const int xa = min(max(c - 1, 0), W - 1), xb = min(c, W - 1);
+    const int ya = min(max(r - 1, 0), H - 1), yb = min(r, H - 1);
+    const float t00 = src[ya * spitch + xa], t01 = src[yb * spitch + xa];
+    const float t10 = src[ya * spitch + xb], t11 = src[yb * spitch + xb];
+    const bool ok = t00 >= 0.0f && t00 <= 255.0f && t00 == dm_floor(t00) && (__float_as_uint(t00) >> 31) == 0u;
+    if (!ok) *not_u8 = 1u;
+    auto b = [](float t) -> uint32_t { return (t >= 0.0f && t <= 255.0f) ? (uint32_t)t : 0u; };
+    dst[(size_t)r * dpitch + c] = b(t00) | (b(t01) << 8) | (b(t10) << 16) | (b(t11) << 24);
+}
+
+hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch, uint32_t *not_u8,
+                           hipStream_t s) {
+    dim3 block(64, 4), grid((W + 2 + 63) / 64, (H + 2 + 3) / 4);
+    k_pad_quad<<<grid, block, 0, s>>>(src, spitch, W, H, dst, dpitch, not_u8);
+    return hipGetLastError();
+}
+
 int diag_read_cycles(unsigned long long *out8) {
 #ifdef ACMMP_DIAG_STAMPS
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 8 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 16 * sizeof(unsigned long long)) != hipSuccess)
         return -3;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_cycles), z, sizeof(z)) != hipSuccess) return -3;
     return 0;
 #else
@@ -1544,22 +1644,23 @@ static int ns_bucket(int nsrc) {
     return 32;
 }
 
-#define ACMMP_LAUNCH_NSW(KERNEL, W, GRID, BLOCK, STREAM, ...)                              \
+#define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...)                             \
     switch (ns_bucket(h_kv.nsrc)) {                                                         \
-        case 4: KERNEL<4, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;               \
-        case 9: KERNEL<9, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;               \
-        case 16: KERNEL<16, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
-        case 20: KERNEL<20, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
-        default: KERNEL<32, W><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+        case 4: KERNEL<4, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;              \
+        case 9: KERNEL<9, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;              \
+        case 16: KERNEL<16, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
+        case 20: KERNEL<20, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
+        default: KERNEL<32, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
     }
 
 // Source-view count -> array capacity; KViews::wide -> the integer record
-// index of views with 2^24 or more records.
+// index of views with 2^24 or more records; KViews::u8 -> u8 texel quads.
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
-    if (h_kv.wide) {                                                                        \
-        ACMMP_LAUNCH_NSW(KERNEL, true, GRID, BLOCK, STREAM, __VA_ARGS__)                    \
-    } else {                                                                                \
-        ACMMP_LAUNCH_NSW(KERNEL, false, GRID, BLOCK, STREAM, __VA_ARGS__)                   \
+    switch ((h_kv.wide ? kTxWide : 0) | (h_kv.u8 ? kTxU8 : 0)) {                            \
+        case 0: { ACMMP_LAUNCH_NSW(KERNEL, 0, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        case 1: { ACMMP_LAUNCH_NSW(KERNEL, 1, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        case 2: { ACMMP_LAUNCH_NSW(KERNEL, 2, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        default: { ACMMP_LAUNCH_NSW(KERNEL, 3, GRID, BLOCK, STREAM, __VA_ARGS__) } break;   \
     }
 
 static dim3 cs_grid(const KViews &kv, int colours) {

@@ -166,6 +166,10 @@ class ACMMP:
         self._check(self._lib.acmmp_set_images(self._ctx, n, cam_arr, ptrs, int(keep_depth_range)),
                     "acmmp_set_images")
 
+    def texel_bits(self) -> int:
+        """8 when the gathers read u8 texel quads, 32 for fp32 row pairs."""
+        return int(self._lib.acmmp_get_texel_bits(self._ctx))
+
     def set_depth_maps(self, depths: Sequence[np.ndarray]):
         ds = [np.ascontiguousarray(d, dtype=np.float32) for d in depths]
         ptrs = (C.POINTER(C.c_float) * len(ds))(*[_fptr(d) for d in ds])

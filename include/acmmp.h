@@ -284,6 +284,13 @@ int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
  * bit-identical to the pinned division on this device. */
 int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked);
 
+/* Texel storage the gather kernels use for the current images (set by
+ * acmmp_set_images*): 8 = u8 quads (every view integer-valued in [0, 255],
+ * e.g. 8-bit JPEG input at native size), 32 = fp32 row pairs. Results are
+ * identical either way; this reports the memory format only. No reference
+ * counterpart (diagnostic). */
+int acmmp_get_texel_bits(const acmmp_ctx *ctx);
+
 /* Number of visible HIP devices (0 when none / no driver). */
 int acmmp_device_count(void);
 /* Library build string (arch, flags). */
