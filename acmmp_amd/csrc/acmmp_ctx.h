@@ -34,8 +34,8 @@ struct acmmp_ctx {
     std::vector<float *> pad;          // padded source images (KViews::pad), owned
     std::vector<size_t> pad_bytes;
     std::vector<int> pad_pitch;
-    bool pad_u8 = false;               // pad[] hold u8 quads (KViews::u8)
-    uint32_t *d_not_u8 = nullptr;      // device flag of the u8 check
+    int pad_texel = 0;                 // form of pad[] (KViews::texel, kTexel*)
+    uint32_t *d_not_u8 = nullptr;      // device flag: a view does not fit the compact form
     std::vector<int> dep_pitch, dep_w, dep_h;
     bool have_depths = false;
 

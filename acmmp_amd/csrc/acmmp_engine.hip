@@ -121,7 +121,7 @@ int kv_upload(acmmp_ctx *ctx) {
         if ((size_t)ctx->pad_pitch[i] * (ctx->cams[i].height + 2) >= (1u << 24)) kv.wide = 1;
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
-    kv.u8 = ctx->pad_u8 ? 1 : 0;
+    kv.texel = ctx->pad_texel;
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737
@@ -262,21 +262,31 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         ctx->pad_bytes.resize(num_images, 0);
         ctx->pad_pitch.resize(num_images, 0);
     }
-    // First the u8 quad form (4 B per footprint): valid when every view is
-    // integer-valued in [0, 255], which one device flag reports (one stream
-    // sync). Otherwise the fp32 row-paired form (16 B per footprint) is built
-    // over it. ACMMP_TEXEL_F32=1 forces the fp32 form (parity tests of both).
-    bool force_f32 = false;
-    if (const char *e = std::getenv("ACMMP_TEXEL_F32")) force_f32 = e[0] == '1';
+    // The most compact form every view fits, each attempt checked by one
+    // device flag (one stream sync): u8 quads (4 B per footprint: every view
+    // integer-valued in [0, 255]), then f16 difference quads (8 B: every
+    // stored value exact in f16), else the fp32 row-paired form (16 B).
+    // ACMMP_TEXEL=u8|h16|f32 restricts the attempt to that one form before
+    // fp32 (ACMMP_TEXEL_F32=1 = f32): the parity tests of every form.
+    int tries[2] = {kTexelU8, kTexelH16}, ntry = 2;
+    if (const char *e = std::getenv("ACMMP_TEXEL")) {
+        if (!std::strcmp(e, "f32")) ntry = 0;
+        else if (!std::strcmp(e, "u8")) ntry = 1;
+        else if (!std::strcmp(e, "h16")) { tries[0] = kTexelH16; ntry = 1; }
+    }
+    if (const char *e = std::getenv("ACMMP_TEXEL_F32"))
+        if (e[0] == '1') ntry = 0;
     if (!ctx->d_not_u8) HIP_TRY(ctx, dalloc(ctx->d_not_u8, 1));
-    for (int pass = force_f32 ? 1 : 0; pass < 2; ++pass) {
-        if (pass == 0) HIP_TRY(ctx, hipMemsetAsync(ctx->d_not_u8, 0, sizeof(uint32_t), ctx->stream));
+    ctx->pad_texel = -1;
+    for (int k = 0; k <= ntry && ctx->pad_texel < 0; ++k) {
+        const int form = k < ntry ? tries[k] : kTexelF32;
+        if (form != kTexelF32) HIP_TRY(ctx, hipMemsetAsync(ctx->d_not_u8, 0, sizeof(uint32_t), ctx->stream));
         for (int i = 0; i < num_images; ++i) {
             const int w = cams[i].width, h = cams[i].height;
-            // records per row: u8 quads (W + 2, 128-B rows) or fp32 row pairs
-            // (W + 3, 128-B rows); the f32 form is the larger allocation
-            const int pq = (w + 2 + 31) / 32 * 32, pf = (w + 3 + 15) / 16 * 16;
-            const int pp = pass == 0 ? pq : pf;
+            // records per row (128-B rows): u8 quads W + 2, f16 quads W + 2,
+            // fp32 row pairs W + 3; the f32 form is the largest allocation
+            const int pf = (w + 3 + 15) / 16 * 16;
+            const int pp = form == kTexelU8 ? (w + 2 + 31) / 32 * 32 : form == kTexelH16 ? (w + 2 + 15) / 16 * 16 : pf;
             const size_t bytes = (size_t)pf * (h + 2) * 2 * sizeof(float);
             // the gather kernels index records with a 24x24-bit multiply into a
             // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
@@ -289,21 +299,23 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
                 ctx->pad_bytes[i] = bytes;
             }
             ctx->pad_pitch[i] = pp;
-            if (pass == 0)
+            if (form == kTexelF32)
+                HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
+            else if (form == kTexelU8)
                 HIP_TRY(ctx, launch_pad_quad(ctx->img[i], ctx->img_pitch[i], w, h,
                                              reinterpret_cast<uint32_t *>(ctx->pad[i]), pp, ctx->d_not_u8,
                                              ctx->stream));
             else
-                HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
+                HIP_TRY(ctx, launch_pad_h16(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->d_not_u8,
+                                            ctx->stream));
         }
-        if (pass == 0) {
-            uint32_t not_u8 = 1;
-            HIP_TRY(ctx, hipMemcpyAsync(&not_u8, ctx->d_not_u8, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            ctx->pad_u8 = not_u8 == 0;
-            if (ctx->pad_u8) break;
+        if (form == kTexelF32) {
+            ctx->pad_texel = kTexelF32;
         } else {
-            ctx->pad_u8 = false;
+            uint32_t unfit = 1;
+            HIP_TRY(ctx, hipMemcpyAsync(&unfit, ctx->d_not_u8, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (unfit == 0) ctx->pad_texel = form;
         }
     }
     if (resize || !ctx->d_rm_plane) {
@@ -377,7 +389,7 @@ int acmmp_device_count(void) {
 
 int acmmp_get_texel_bits(const acmmp_ctx *ctx) {
     if (!ctx) return ACMMP_ERR_ARG;
-    return ctx->pad_u8 ? 8 : 32;
+    return ctx->pad_texel == kTexelU8 ? 8 : ctx->pad_texel == kTexelH16 ? 16 : 32;
 }
 
 const char *acmmp_version(void) {

@@ -30,6 +30,9 @@ struct ViewRel {
     float tr[3];   // t_relative
 };
 
+// Texel forms of the padded source views (KViews::texel).
+enum { kTexelF32 = 0, kTexelU8 = 1, kTexelH16 = 2 };
+
 struct KViews {
     acmmp_params prm;
     acmmp_camera cam[ACMMP_MAX_IMAGES];
@@ -39,9 +42,13 @@ struct KViews {
     // Source images with clamp-to-edge baked in, so the 2x2 bilinear
     // footprint of a coordinate clamped to [-1, W] x [-1, H] is ONE load at
     // record (y0 + 1, x0 + 1), without integer clamps or selects. Either
-    //  * u8 quads (u8 = 1): record (r, c), r < H + 2, c < W + 2, packs the
-    //    bytes of texels (c-1, r-1), (c-1, r), (c, r-1), (c, r) (clamped):
-    //    4 B per footprint, when every view is integer-valued in [0, 255];
+    //  * f16 difference quads (kTexelH16): record (r, c), r < H + 2,
+    //    c < W + 2, holds the halves (t00, t01, t10 - t00, t11 - t01) of
+    //    texels t00 = (c-1, r-1), t01 = (c-1, r), t10 = (c, r-1),
+    //    t11 = (c, r) (clamped): 8 B per footprint, when every stored value
+    //    is exact in f16 (8-bit input is);
+    //  * u8 quads (kTexelU8): the bytes of the same four texels, 4 B per
+    //    footprint, when every view is integer-valued in [0, 255];
     //  * fp32 row pairs: record (r, c), c < W + 3, is the float pair
     //    (texel(c-1, r-1), texel(c-1, r)); a footprint is two records, 16 B.
     const float *pad[ACMMP_MAX_IMAGES];
@@ -52,7 +59,7 @@ struct KViews {
     int dh[ACMMP_MAX_IMAGES];
     int W, H, Wh, sweep_rows, nsrc;
     int wide;                                 // some view has >= 2^24 padded records
-    int u8;                                   // pad[] hold u8 texel quads (every view integer-valued 0..255)
+    int texel;                                // form of pad[]: kTexelF32 / kTexelU8 / kTexelH16
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
 };
@@ -89,6 +96,10 @@ hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4
 
 hipError_t launch_pad_image(const float *src, int spitch, int W, int H, float *dst, int dpitch,
                             hipStream_t stream);
+// f16 difference-quad copy of one view; sets *not_h16 = 1 if a stored value
+// is not exact in f16 (the copy is then unusable and the fp32 form is built).
+hipError_t launch_pad_h16(const float *src, int spitch, int W, int H, void *dst, int dpitch, uint32_t *not_h16,
+                          hipStream_t stream);
 // u8 texel-quad copy of one view; sets *not_u8 = 1 if a texel is not an
 // integer in [0, 255] (the copy is then unusable and the fp32 form is built).
 hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch,

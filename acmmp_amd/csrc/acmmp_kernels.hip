@@ -35,6 +35,9 @@ constexpr int kTaps = 6;
 
 // Minimum waves per SIMD the sweep kernel is register-allocated for
 // (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
+#ifndef ACMMP_PIPE_ROWS
+#define ACMMP_PIPE_ROWS 1
+#endif
 #ifndef ACMMP_SWEEP_WAVES
 #define ACMMP_SWEEP_WAVES 2
 #endif
@@ -276,7 +279,12 @@ DEV float2 project(const float *H, float x, float y) {
 //          input at native size is): one 4-byte record per bilinear
 //          footprint instead of 16 bytes; v_cvt_f32_ubyte* restores the exact
 //          fp32 texel values, so the arithmetic is unchanged.
-constexpr int kTxWide = 1, kTxU8 = 2;
+//   bit 2 (kTxH16):  the padded source views hold f16 "difference quads"
+//          (t00, t01, t10 - t00, t11 - t01) for views whose every stored value
+//          is exact in f16 (8-bit input is): 8 bytes per footprint, and the
+//          two row lerps are v_fma_mix_f32 straight from the f16 halves (the
+//          f16 -> f32 widening is exact, the fma is the pinned fp32 fma).
+constexpr int kTxWide = 1, kTxU8 = 2, kTxH16 = 4;
 
 // Source-image sampler: one buffer resource (SRD) per view over the padded
 // copy (KViews::pad), built from wave-uniform values (the view index is a
@@ -342,8 +350,21 @@ constexpr int kPairs = kTaps / 2;
 constexpr int kSlots = kPairs * kTaps;
 DEV int wslot(int p, int jj) { return jj * kPairs + p; }
 
+// ACMMP_LDS_WR=1: slots hold (w_a, w_b, w_a*ref_a, w_b*ref_b) as float4
+// (72 KB per block, one ds_read_b128 per pair and no w*ref product in the
+// sample loop); 0: (w_a, w_b) float2 with the reference pair read from the
+// tile (36 KB per block).
+#ifndef ACMMP_LDS_WR
+#define ACMMP_LDS_WR 0
+#endif
+#if ACMMP_LDS_WR
+typedef float4 WSlot;
+#else
+typedef float2 WSlot;
+#endif
+
 struct PixPatch {
-    float2 *w;       // LDS: slot k of this lane at [k * kThreads]
+    WSlot *w;        // LDS: slot k of this lane at [k * kThreads]
     const float *rt; // LDS: this lane's first reference sample in the tile (tile + tb)
     int wo;          // this lane's offset into the weight array (w = wbase + wo)
     float mean;      // sum_ref * inv_bilateral_weight_sum
@@ -381,6 +402,9 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_w += w;
             float *slot = reinterpret_cast<float *>(&pp.w[wslot(ii >> 1, jj) * kThreads]);
             slot[ii & 1] = w;
+#if ACMMP_LDS_WR
+            slot[2 + (ii & 1)] = wr;
+#endif
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -401,6 +425,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // (address = base + vindex * stride + voffset); clang has no builtin for it.
 __device__ u32x4 amdgcn_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                 int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ u32x2 amdgcn_struct_buffer_load_b64(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                                               int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
 __device__ unsigned amdgcn_struct_buffer_load_b32(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                   int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
 
@@ -423,21 +451,157 @@ DEV float lerp_sample(u32x4 t, float ax, float ay) {
     return dm_fma(ay, tb.y - tb.x, tb.x);
 }
 
+// One patch row's gathers in flight: the fetched footprints (in the form
+// of TX) and the bilinear fractions of the row's 6 samples.
+template <int TX>
+struct RowFetch {
+    u32x4 t[kTaps];   // fp32 row pairs
+    unsigned q[kTaps];  // u8 quads
+    u32x2 hq[kTaps];  // f16 difference quads
+    f2v ax[kPairs], ay[kPairs];
+};
+
+// Projection, clamp, fractions and record index of patch row jj, and its 6
+// loads issued (not waited for).
+template <bool FAST, int TX>
+DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
+                   RowFetch<TX> &rf) {
+    constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
+    const f2v fw = splat((float)im.W), fh = splat((float)im.H);
+    const f2v y = splat((float)(py - 5 + 2 * jj));
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) {
+        const f2v hx = fma2(splat(H[1]), y, cx[p]);
+        const f2v hy = fma2(splat(H[4]), y, cy[p]);
+        const f2v hz = fma2(splat(H[7]), y, cz[p]);
+        f2v inv;
+        if (FAST) {  // v_rcp + one Newton step == IEEE 1/z in the window
+            const f2v r = f2v{__builtin_amdgcn_rcpf(hz.x), __builtin_amdgcn_rcpf(hz.y)};
+            inv = fma2(fma2(-hz, r, splat(1.0f)), r, r);
+        } else {
+            inv = f2v{1.0f / hz.x, 1.0f / hz.y};
+        }
+        f2v u = hx * inv, v = hy * inv;
+        u = (u + 0.5f) - 0.5f;
+        v = (v + 0.5f) - 0.5f;
+        // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
+        // (finite homography, |hz| inside the reciprocal window), where
+        // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
+        // bounds are never +-0) == the oracle's selects.
+        f2v xs, ys;
+        if (FAST) {
+            xs = f2v{__builtin_amdgcn_fmed3f(u.x, -1.0f, fw.x), __builtin_amdgcn_fmed3f(u.y, -1.0f, fw.x)};
+            ys = f2v{__builtin_amdgcn_fmed3f(v.x, -1.0f, fh.x), __builtin_amdgcn_fmed3f(v.y, -1.0f, fh.x)};
+        } else {
+            xs = f2v{fminf(fmaxf(u.x, -1.0f), fw.x), fminf(fmaxf(u.y, -1.0f), fw.x)};
+            ys = f2v{fminf(fmaxf(v.x, -1.0f), fh.x), fminf(fmaxf(v.y, -1.0f), fh.x)};
+        }
+        const f2v flx = f2v{dm_floor(xs.x), dm_floor(xs.y)};
+        const f2v fly = f2v{dm_floor(ys.x), dm_floor(ys.y)};
+        rf.ax[p] = xs - flx;
+        rf.ay[p] = ys - fly;
+        // record index (y0 + 1) * pitch + x0 + 1
+        unsigned ia, ib;
+        if (!WIDE) {
+            // = fma(y0, pitch, x0 + pitch + 1): integers below 2^24, so
+            // exact in fp32 (the engine selects WIDE otherwise)
+            const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
+            ia = (unsigned)idx.x;
+            ib = (unsigned)idx.y;
+        } else {
+            // views of 2^24 records or more: integer multiply-add (24-bit
+            // operands, 32-bit result)
+            const f2v q = flx + 1.0f, r = fly + 1.0f;
+            ia = __umul24((unsigned)r.x, (unsigned)im.pitch) + (unsigned)q.x;
+            ib = __umul24((unsigned)r.y, (unsigned)im.pitch) + (unsigned)q.y;
+        }
+        if (H16) {
+            rf.hq[2 * p] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ia, 0, 0, 0);
+            rf.hq[2 * p + 1] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ib, 0, 0, 0);
+        } else if (U8) {
+#ifdef ACMMP_DIAG_NOGATHER  // timing experiment only: no memory access
+            rf.q[2 * p] = ia * 0x01010101u;
+            rf.q[2 * p + 1] = ib * 0x01010101u;
+#else
+            rf.q[2 * p] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ia, 0, 0, 0);
+            rf.q[2 * p + 1] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ib, 0, 0, 0);
+#endif
+        } else {
+            rf.t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
+            rf.t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
+        }
+    }
+}
+
+// Bilinear values of a fetched row and their weighted sums into the
+// per-column accumulators (w from the LDS weight slots, ref from the tile).
+template <int TX>
+DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, int wstride, int jj, f2v *acc_s,
+                    f2v *acc_ss, f2v *acc_rs) {
+    constexpr bool U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) {
+        f2v sv;
+        if (H16) {
+            // row lerps fma(ax, t1x - t0x, t0x) as v_fma_mix_f32 on the
+            // halves, then the column lerp of both samples packed (words
+            // copied out first: clang's __builtin_bit_cast of a
+            // vector-element lvalue reads element 0)
+            const unsigned wa0 = rf.hq[2 * p].x, wa1 = rf.hq[2 * p].y;
+            const unsigned wb0 = rf.hq[2 * p + 1].x, wb1 = rf.hq[2 * p + 1].y;
+            const h2v ta = __builtin_bit_cast(h2v, wa0), da = __builtin_bit_cast(h2v, wa1);
+            const h2v tb = __builtin_bit_cast(h2v, wb0), db = __builtin_bit_cast(h2v, wb1);
+            const f2v r0 = f2v{__builtin_fmaf(rf.ax[p].x, (float)da.x, (float)ta.x),
+                               __builtin_fmaf(rf.ax[p].y, (float)db.x, (float)tb.x)};
+            const f2v r1 = f2v{__builtin_fmaf(rf.ax[p].x, (float)da.y, (float)ta.y),
+                               __builtin_fmaf(rf.ax[p].y, (float)db.y, (float)tb.y)};
+            sv = fma2(rf.ay[p], r1 - r0, r0);
+        } else if (U8) {
+            sv = f2v{lerp_sample(unpack_quad(rf.q[2 * p]), rf.ax[p].x, rf.ay[p].x),
+                     lerp_sample(unpack_quad(rf.q[2 * p + 1]), rf.ax[p].y, rf.ay[p].y)};
+        } else {
+            sv = f2v{lerp_sample(rf.t[2 * p], rf.ax[p].x, rf.ay[p].x),
+                     lerp_sample(rf.t[2 * p + 1], rf.ax[p].y, rf.ay[p].y)};
+        }
+        // w from the weight slots, ref from the tile: w * ref is the same
+        // IEEE product pixel_patch formed, so re-forming it is exact
+#ifdef ACMMP_DIAG_NOLDS  // timing experiment only: no LDS reads in the sample loop
+        const float2 w = make_float2(rf.ax[p].x, rf.ay[p].y);
+        const float rr[2] = {rf.ax[p].y, rf.ay[p].x};
+#else
+        const WSlot w = wl[wslot(p, jj) * wstride];
+#if !ACMMP_LDS_WR
+        const float *rr = rt + 2 * kTileW * jj + 2 * p;
+#endif
+#endif
+        const f2v wv = f2v{w.x, w.y};
+#if ACMMP_LDS_WR && !defined(ACMMP_DIAG_NOLDS)
+        const f2v wr = f2v{w.z, w.w};
+#else
+        const f2v wr = wv * f2v{rr[0], rr[1]};
+#endif
+        const f2v ws = wv * sv;
+        acc_s[p] += ws;
+        acc_ss[p] = fma2(ws, sv, acc_ss[p]);
+        acc_rs[p] = fma2(wr, sv, acc_rs[p]);
+    }
+}
+
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412).
 //
 // Per sample: projection (pin P1, the x-terms hoisted per column), the
-// coordinate clamp of pin P2, and ONE 16-byte load of the 2x2 bilinear
-// footprint from the row-paired padded image (element (r, c) holds the
-// texels of rows r-1 and r at column c-1, clamp-to-edge, so the load at
-// (y0 + 1, x0 + 1) returns texels (x0,y0), (x0,y0+1), (x0+1,y0), (x0+1,y0+1)).
+// coordinate clamp of pin P2, and ONE load of the 2x2 bilinear footprint
+// from the padded source view (KViews::pad) at record (y0 + 1, x0 + 1).
 //
 // Rows are gathered one at a time (a lane's 6 samples of a row sit in the
-// same one or two cache lines, which matters when neighbouring lanes'
-// hypotheses are incoherent) and accumulated into per-column partial sums:
-// within a column the rows are still added in order jj = 0..5, columns are
-// summed at the end in order ii — the pinned order (src/ACMMP.cu:382-412).
+// same one or two cache lines) and accumulated into per-column partial
+// sums: within a column the rows are still added in order jj = 0..5,
+// columns are summed at the end in order ii — the pinned order
+// (src/ACMMP.cu:382-412). The row loop is software-pipelined: row jj + 1's
+// loads are issued before row jj is reduced, so a row's gather latency
+// overlaps the previous row's arithmetic.
 template <bool FAST, int TX>
-DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, const float *rt, int wstride, int px,
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, const float *rt, int wstride, int px,
                        int py, float &sum_src, float &sum_ss, float &sum_rs) {
     f2v cx[kPairs], cy[kPairs], cz[kPairs];
 #pragma unroll
@@ -447,102 +611,30 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const float2 *wl, con
         cy[p] = fma2(splat(H[3]), x, splat(H[5]));
         cz[p] = fma2(splat(H[6]), x, splat(H[8]));
     }
-    constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0;
     f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
-    const f2v fw = splat((float)im.W), fh = splat((float)im.H);
+#if ACMMP_PIPE_ROWS
+    // two rows per trip (ping-pong fetch buffers, no register copies)
+    RowFetch<TX> ra, rb;
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
+#pragma unroll 1
+    for (int jj = 0; jj < kTaps; jj += 2) {
+        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 1, rb);
+        reduce_row<TX>(ra, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
+        if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 2, ra);
+        reduce_row<TX>(rb, wl, rt, wstride, jj + 1, acc_s, acc_ss, acc_rs);
+    }
+#else
     // rows are a rolled loop: one row's 6 gathers in flight, reduced, next row
     // (unrolling lets the compiler hoist every row's address math and spill)
 #pragma unroll 1
     for (int jj = 0; jj < kTaps; ++jj) {
-        const f2v y = splat((float)(py - 5 + 2 * jj));
-        u32x4 t[kTaps];
-        unsigned q[kTaps];
-        f2v ax[kPairs], ay[kPairs];
-#pragma unroll
-        for (int p = 0; p < kPairs; ++p) {
-            const f2v hx = fma2(splat(H[1]), y, cx[p]);
-            const f2v hy = fma2(splat(H[4]), y, cy[p]);
-            const f2v hz = fma2(splat(H[7]), y, cz[p]);
-            f2v inv;
-            if (FAST) {  // v_rcp + one Newton step == IEEE 1/z in the window
-                const f2v r = f2v{__builtin_amdgcn_rcpf(hz.x), __builtin_amdgcn_rcpf(hz.y)};
-                inv = fma2(fma2(-hz, r, splat(1.0f)), r, r);
-            } else {
-                inv = f2v{1.0f / hz.x, 1.0f / hz.y};
-            }
-            f2v u = hx * inv, v = hy * inv;
-            u = (u + 0.5f) - 0.5f;
-            v = (v + 0.5f) - 0.5f;
-            // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
-            // (finite homography, |hz| inside the reciprocal window), where
-            // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
-            // bounds are never +-0) == the oracle's selects.
-            f2v xs, ys;
-            if (FAST) {
-                xs = f2v{__builtin_amdgcn_fmed3f(u.x, -1.0f, fw.x), __builtin_amdgcn_fmed3f(u.y, -1.0f, fw.x)};
-                ys = f2v{__builtin_amdgcn_fmed3f(v.x, -1.0f, fh.x), __builtin_amdgcn_fmed3f(v.y, -1.0f, fh.x)};
-            } else {
-                xs = f2v{fminf(fmaxf(u.x, -1.0f), fw.x), fminf(fmaxf(u.y, -1.0f), fw.x)};
-                ys = f2v{fminf(fmaxf(v.x, -1.0f), fh.x), fminf(fmaxf(v.y, -1.0f), fh.x)};
-            }
-            const f2v flx = f2v{dm_floor(xs.x), dm_floor(xs.y)};
-            const f2v fly = f2v{dm_floor(ys.x), dm_floor(ys.y)};
-            ax[p] = xs - flx;
-            ay[p] = ys - fly;
-            // record index (y0 + 1) * pitch + x0 + 1
-            unsigned ia, ib;
-            if (!WIDE) {
-                // = fma(y0, pitch, x0 + pitch + 1): integers below 2^24, so
-                // exact in fp32 (the engine selects WIDE otherwise)
-                const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
-                ia = (unsigned)idx.x;
-                ib = (unsigned)idx.y;
-            } else {
-                // views of 2^24 records or more: integer multiply-add (24-bit
-                // operands, 32-bit result)
-                const f2v q = flx + 1.0f, r = fly + 1.0f;
-                ia = __umul24((unsigned)r.x, (unsigned)im.pitch) + (unsigned)q.x;
-                ib = __umul24((unsigned)r.y, (unsigned)im.pitch) + (unsigned)q.y;
-            }
-            if (U8) {
-#ifdef ACMMP_DIAG_NOGATHER  // timing experiment only: no memory access
-                q[2 * p] = ia * 0x01010101u;
-                q[2 * p + 1] = ib * 0x01010101u;
-#else
-                q[2 * p] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ia, 0, 0, 0);
-                q[2 * p + 1] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ib, 0, 0, 0);
-#endif
-            } else {
-                t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
-                t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < kPairs; ++p) {
-            if (U8) {
-                t[2 * p] = unpack_quad(q[2 * p]);
-                t[2 * p + 1] = unpack_quad(q[2 * p + 1]);
-            }
-            const f2v sv = f2v{lerp_sample(t[2 * p], ax[p].x, ay[p].x), lerp_sample(t[2 * p + 1], ax[p].y, ay[p].y)};
-            // w from the weight slots, ref from the tile: w * ref is the same
-            // IEEE product pixel_patch formed, so re-forming it is exact
-#ifdef ACMMP_DIAG_NOLDS  // timing experiment only: no LDS reads in the sample loop
-            const float2 w = make_float2(ax[p].x, ay[p].y);
-            const float rr[2] = {ax[p].y, ay[p].x};
-#else
-            const float2 w = wl[wslot(p, jj) * wstride];
-            const float *rr = rt + 2 * kTileW * jj + 2 * p;
-#endif
-            const f2v wv = f2v{w.x, w.y};
-            const f2v wr = wv * f2v{rr[0], rr[1]};
-            const f2v ws = wv * sv;
-            acc_s[p] += ws;
-            acc_ss[p] = fma2(ws, sv, acc_ss[p]);
-            acc_rs[p] = fma2(wr, sv, acc_rs[p]);
-        }
+        RowFetch<TX> rf;
+        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj, rf);
+        reduce_row<TX>(rf, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
     }
+#endif
     sum_src = 0.0f;
     sum_ss = 0.0f;
     sum_rs = 0.0f;
@@ -567,7 +659,7 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     // stays visible and the reads are ds_read, not flat)
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
-    const float2 *wl = pp.w - pp.wo + wo;
+    const WSlot *wl = pp.w - pp.wo + wo;
     ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
@@ -818,7 +910,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
 template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSlots * kThreads];
+    __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -910,7 +1002,7 @@ template <int NS, int TX>
 __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSlots * kThreads];
+    __shared__ WSlot wlds[kSlots * kThreads];
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -1470,7 +1562,7 @@ template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
-    __shared__ float2 wlds[kSlots * kThreads];
+    __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block();
@@ -1544,6 +1636,41 @@ __global__ __launch_bounds__(256) void k_pad_quad(const float *__restrict__ src,
     if (!ok) *not_u8 = 1u;
     auto b = [](float t) -> uint32_t { return (t >= 0.0f && t <= 255.0f) ? (uint32_t)t : 0u; };
     dst[(size_t)r * dpitch + c] = b(t00) | (b(t01) << 8) | (b(t10) << 16) | (b(t11) << 24);
+}
+
+// f16 difference-quad layout: element (r, c), r < H + 2, c < W + 2, holds
+// the halves (t00, t01, t10 - t00, t11 - t01) of the same clamped texels as
+// the u8 quad, the differences formed in fp32 exactly as the lerp forms them
+// (lerp_sample). Sets *not_h16 if any stored value is not exactly
+// representable (non-finite, beyond +-65504, or more than 11 significant
+// bits); the copy is then unusable and the fp32 form is built.
+__global__ __launch_bounds__(256) void k_pad_h16(const float *__restrict__ src, int spitch, int W, int H,
+                                                 uint2 *__restrict__ dst, int dpitch, uint32_t *not_h16) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int r = blockIdx.y * 4 + threadIdx.y;
+    if (c >= W + 2 || r >= H + 2) return;
+    const int xa = min(max(c - 1, 0), W - 1), xb = min(c, W - 1);
+    const int ya = min(max(r - 1, 0), H - 1), yb = min(r, H - 1);
+    const float t00 = src[ya * spitch + xa], t01 = src[yb * spitch + xa];
+    const float t10 = src[ya * spitch + xb], t11 = src[yb * spitch + xb];
+    const float v[4] = {t00, t01, t10 - t00, t11 - t01};
+    _Float16 h[4];
+    bool ok = true;
+    for (int i = 0; i < 4; ++i) {
+        h[i] = (_Float16)v[i];
+        const float back = (float)h[i];
+        ok = ok && __float_as_uint(back) == __float_as_uint(v[i]) && dm_fabs(v[i]) <= 65504.0f;
+    }
+    if (!ok) *not_h16 = 1u;
+    dst[(size_t)r * dpitch + c] = make_uint2(__builtin_bit_cast(uint32_t, h2v{h[0], h[1]}),
+                                             __builtin_bit_cast(uint32_t, h2v{h[2], h[3]}));
+}
+
+hipError_t launch_pad_h16(const float *src, int spitch, int W, int H, void *dst, int dpitch, uint32_t *not_h16,
+                          hipStream_t s) {
+    dim3 block(64, 4), grid((W + 2 + 63) / 64, (H + 2 + 3) / 4);
+    k_pad_h16<<<grid, block, 0, s>>>(src, spitch, W, H, reinterpret_cast<uint2 *>(dst), dpitch, not_h16);
+    return hipGetLastError();
 }
 
 hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch, uint32_t *not_u8,
@@ -1654,13 +1781,16 @@ static int ns_bucket(int nsrc) {
     }
 
 // Source-view count -> array capacity; KViews::wide -> the integer record
-// index of views with 2^24 or more records; KViews::u8 -> u8 texel quads.
+// index of views with 2^24 or more records; KViews::texel -> the texel form.
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
-    switch ((h_kv.wide ? kTxWide : 0) | (h_kv.u8 ? kTxU8 : 0)) {                            \
+    switch ((h_kv.wide ? kTxWide : 0) | (h_kv.texel == kTexelU8 ? kTxU8 : 0) |              \
+            (h_kv.texel == kTexelH16 ? kTxH16 : 0)) {                                       \
         case 0: { ACMMP_LAUNCH_NSW(KERNEL, 0, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 1: { ACMMP_LAUNCH_NSW(KERNEL, 1, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 2: { ACMMP_LAUNCH_NSW(KERNEL, 2, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        default: { ACMMP_LAUNCH_NSW(KERNEL, 3, GRID, BLOCK, STREAM, __VA_ARGS__) } break;   \
+        case 3: { ACMMP_LAUNCH_NSW(KERNEL, 3, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        case 4: { ACMMP_LAUNCH_NSW(KERNEL, 4, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        default: { ACMMP_LAUNCH_NSW(KERNEL, 5, GRID, BLOCK, STREAM, __VA_ARGS__) } break;   \
     }
 
 static dim3 cs_grid(const KViews &kv, int colours) {

@@ -167,7 +167,8 @@ class ACMMP:
                     "acmmp_set_images")
 
     def texel_bits(self) -> int:
-        """8 when the gathers read u8 texel quads, 32 for fp32 row pairs."""
+        """16 when the gathers read f16 difference quads, 8 for u8 quads, 32
+        for fp32 row pairs (acmmp_get_texel_bits)."""
         return int(self._lib.acmmp_get_texel_bits(self._ctx))
 
     def set_depth_maps(self, depths: Sequence[np.ndarray]):

@@ -285,10 +285,12 @@ int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
 int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked);
 
 /* Texel storage the gather kernels use for the current images (set by
- * acmmp_set_images*): 8 = u8 quads (every view integer-valued in [0, 255],
- * e.g. 8-bit JPEG input at native size), 32 = fp32 row pairs. Results are
- * identical either way; this reports the memory format only. No reference
- * counterpart (diagnostic). */
+ * acmmp_set_images*): 16 = f16 difference quads (the default whenever every
+ * stored value is exact in f16, e.g. 8-bit JPEG input), 8 = u8 quads (on
+ * request, ACMMP_TEXEL=u8, every view integer-valued in [0, 255]), 32 = fp32
+ * row pairs (any other input, or ACMMP_TEXEL=f32). Results are identical in
+ * every form; this reports the memory format only. No reference counterpart
+ * (diagnostic). */
 int acmmp_get_texel_bits(const acmmp_ctx *ctx);
 
 /* Number of visible HIP devices (0 when none / no driver). */

@@ -1,9 +1,11 @@
-"""Texel storage of the gather kernels (acmmp_kernels.hip, TX template bits):
-u8 quads (4 B per bilinear footprint) when every view is integer-valued in
-[0, 255], fp32 row pairs otherwise. The choice changes the memory format
-only: both must be bit-identical to the oracle, and the automatic choice must
-fall back to fp32 for any view that u8 cannot hold exactly (fractional
-values, out-of-range values, -0.0, NaN).
+"""Texel storage of the gather kernels (acmmp_kernels.hip, TX template bits),
+the most compact form every view fits: u8 quads (4 B per bilinear footprint)
+when every view is integer-valued in [0, 255], else f16 difference quads
+(8 B) when every stored value (texels and the fp32 row differences) is exact
+in f16, else fp32 row pairs (16 B). ACMMP_TEXEL=u8|h16|f32 restricts the
+attempt to one form. The choice changes the memory format only: every form must
+be bit-identical to the oracle, and the automatic choice must fall back to
+fp32 for any view the compact form cannot hold exactly.
 """
 import numpy as np
 import pytest
@@ -44,40 +46,71 @@ def prob():
     return sc.problem(0, 5)
 
 
-@pytest.mark.parametrize("force_f32", [False, True])
-def test_both_texel_forms_match_oracle(prob, monkeypatch, force_f32):
+@pytest.mark.parametrize("form,bits", [(None, 8), ("h16", 16), ("u8", 8), ("f32", 32)])
+def test_every_texel_form_matches_oracle(prob, monkeypatch, form, bits):
     cams, imgs = prob
-    if force_f32:
-        monkeypatch.setenv("ACMMP_TEXEL_F32", "1")
-    bits, prm, pl, co, sv = _run(cams, imgs)
-    assert bits == (32 if force_f32 else 8)
+    if form is not None:
+        monkeypatch.setenv("ACMMP_TEXEL", form)
+    got, prm, pl, co, sv = _run(cams, imgs)
+    assert got == bits
     _check(prm, cams, imgs, pl, co, sv, f"{bits}-bit texels")
 
 
-@pytest.mark.parametrize("kind", ["fraction", "above_255", "negative_zero", "nan"])
-def test_non_u8_views_fall_back_to_f32(prob, kind):
+def test_texel_f32_switch(prob, monkeypatch):
     cams, imgs = prob
+    monkeypatch.setenv("ACMMP_TEXEL_F32", "1")
+    assert _run(cams, imgs)[0] == 32
+
+
+def _perturb(imgs, kind):
     imgs = [im.copy() for im in imgs]
     tgt = imgs[3]  # one source view decides for the whole problem
-    if kind == "fraction":
+    if kind == "quarter":          # exact in f16, not u8
         tgt[10:20, 10:20] += 0.25
-    elif kind == "above_255":
+    elif kind == "third":          # exact in neither
+        tgt[10:20, 10:20] += np.float32(1.0 / 3.0)
+    elif kind == "above_255":      # exact in f16, not u8
         tgt[5, 7] = 256.0
-    elif kind == "negative_zero":
+    elif kind == "beyond_f16":     # above the f16 range
+        tgt[5, 7] = 70000.0
+    elif kind == "odd_4097":       # an integer f16 cannot hold (13 bits)
+        tgt[5, 7] = 4097.0
+    elif kind == "negative_zero":  # f16 holds -0.0, u8 does not
         tgt[tgt == 0] = 0.0
         tgt[0, 0] = -0.0
+    elif kind == "inf":
+        tgt[30, 31] = np.inf
     else:
         tgt[40, 50] = np.nan
+    return imgs
+
+
+# (perturbation, bits when h16 is tried, bits when u8 is tried)
+CASES = [("quarter", 16, 32), ("third", 32, 32), ("above_255", 16, 32), ("beyond_f16", 32, 32),
+         ("odd_4097", 32, 32), ("negative_zero", 16, 32), ("inf", 32, 32), ("nan", 32, 32)]
+
+
+@pytest.mark.parametrize("kind,bits_h16,bits_u8", CASES)
+@pytest.mark.parametrize("form", [None, "h16", "u8"])
+def test_views_the_compact_form_cannot_hold(prob, monkeypatch, kind, bits_h16, bits_u8, form):
+    cams, imgs = prob
+    imgs = _perturb(imgs, kind)
+    if form is not None:
+        monkeypatch.setenv("ACMMP_TEXEL", form)
     bits, prm, pl, co, sv = _run(cams, imgs)
-    assert bits == 32
-    _check(prm, cams, imgs, pl, co, sv, kind)
+    # the default chain tries u8, then h16
+    want = {"h16": bits_h16, "u8": bits_u8, None: bits_u8 if bits_u8 != 32 else bits_h16}[form]
+    assert bits == want
+    _check(prm, cams, imgs, pl, co, sv, f"{kind} ({bits}-bit)")
 
 
-def test_u8_quads_at_image_borders():
+@pytest.mark.parametrize("form,bits", [("h16", 16), ("u8", 8)])
+def test_quads_at_image_borders(monkeypatch, form, bits):
     """Clamp-to-edge through the quad records: tiny odd-sized views whose
     patches mostly project outside the source image."""
+    monkeypatch.setenv("ACMMP_TEXEL", form)
     sc = scene.make_scene(num_views=4, width=21, height=17)
     cams, imgs = sc.problem(0, 3)
-    bits, prm, pl, co, sv = _run(cams, imgs, iters=3)
-    assert bits == 8
-    _check(prm, cams, imgs, pl, co, sv, "u8 borders")
+    got, prm, pl, co, sv = _run(cams, imgs, iters=3)
+    assert got == bits
+    _check(prm, cams, imgs, pl, co, sv, f"{form} borders")

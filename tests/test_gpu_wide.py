@@ -41,13 +41,12 @@ def _random_planes(K, H, W, seed):
     return np.concatenate([n, d[..., None]], -1).astype(np.float32)
 
 
-@pytest.fixture(params=["u8", "f32"])
+@pytest.fixture(params=["h16", "u8", "f32"])
 def wide_index(monkeypatch, request):
-    """Forced integer record index, with either texel form (u8 quads / fp32
-    row pairs, tests/test_gpu_texel_modes.py)."""
+    """Forced integer record index, with every texel form (f16 difference
+    quads / u8 quads / fp32 row pairs, tests/test_gpu_texel_modes.py)."""
     monkeypatch.setenv("ACMMP_WIDE_INDEX", "1")
-    if request.param == "f32":
-        monkeypatch.setenv("ACMMP_TEXEL_F32", "1")
+    monkeypatch.setenv("ACMMP_TEXEL", request.param)
 
 
 def test_forced_wide_index_cost_vectors(wide_index):
