@@ -35,6 +35,9 @@ constexpr int kTaps = 6;
 
 // Minimum waves per SIMD the sweep kernel is register-allocated for
 // (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
+#ifndef ACMMP_CAND_LDS
+#define ACMMP_CAND_LDS 1
+#endif
 #ifndef ACMMP_PIPE_ROWS
 #define ACMMP_PIPE_ROWS 1
 #endif
@@ -1003,6 +1006,9 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
                                                   int iter) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
+#if ACMMP_CAND_LDS
+    __shared__ float4 cand_lds[8 * kThreads];
+#endif
     DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
@@ -1169,6 +1175,16 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         same |= (uint32_t)bs << 6;
     }
 #undef CS
+#if ACMMP_CAND_LDS
+    // the 8 winners' planes, fetched once into this lane's LDS slots (the
+    // NCC prologues then read them at LDS latency, not L2's)
+    float4 *cand_slot = cand_lds + threadIdx.y * kBX + threadIdx.x;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+        if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
+    auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
+    auto cand_dyn = cand;
+#else
     auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
     // wave-uniform d: select chain instead of a dynamically indexed (scratch) array
     auto cand_dyn = [&](int d) -> float4 {
@@ -1177,6 +1193,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         for (int e = 1; e < 8; ++e) ci = (d == e) ? cidx[e] : ci;
         return (((same >> d) & 1u) ? plane_same : plane_opp)[ci];
     };
+#endif
 
     DIAG_T(t_search);
     PixPatch pp;
