@@ -35,6 +35,9 @@ constexpr int kTaps = 6;
 
 // Minimum waves per SIMD the sweep kernel is register-allocated for
 // (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
+#ifndef ACMMP_WAVE2D
+#define ACMMP_WAVE2D 4
+#endif
 #ifndef ACMMP_CAND_LDS
 #define ACMMP_CAND_LDS 1
 #endif
@@ -897,13 +900,26 @@ DEV BlockXY xcd_block() {
     return b;
 }
 
+// ACMMP_WAVE2D = R rows per wave (1, 2 or 4): each wave covers 64/R columns
+// x R rows of the block instead of one 64-column row, so its gathers for
+// neighbouring patch rows overlap in the source image (L1 reuse within a
+// wave); the lane -> pixel map is all that changes.
 DEV LaneGeom lane_geom(int colour, BlockXY b) {
     LaneGeom g;
-    g.k = b.bx * kBX + threadIdx.x;
-    g.py = b.by * kBY + threadIdx.y;
+#if ACMMP_WAVE2D > 1
+    static_assert(kBX == 64 && kBY == 4 && (ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4), "2D wave map of 64x4 blocks");
+    constexpr int R = ACMMP_WAVE2D, C = 64 / R;
+    const int tid = threadIdx.y * kBX + threadIdx.x;
+    const int w = tid >> 6, l = tid & 63;
+    const int tx = (w % R) * C + (l % C), ty = (w / R) * R + l / C;
+#else
+    const int tx = threadIdx.x, ty = threadIdx.y;
+#endif
+    g.k = b.bx * kBX + tx;
+    g.py = b.by * kBY + ty;
     g.s = (g.py + colour) & 1;
     g.px = 2 * g.k + g.s;
-    g.tb = threadIdx.y * kTileW + threadIdx.x + g.s;
+    g.tb = ty * kTileW + tx + g.s;
     return g;
 }
 
