@@ -33,17 +33,29 @@ namespace acmmp {
 // offsets {-5,-3,-1,1,3,5}^2, src/ACMMP.h:34,37). The engine rejects others.
 constexpr int kTaps = 6;
 
-// Minimum waves per SIMD the sweep kernel is register-allocated for
-// (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
+// Build options of the gather kernels (each an A/B-measured choice; the
+// defaults are the measured winners):
+//   ACMMP_WAVE2D         rows of pixels per wave (lane_geom_of)
+//   ACMMP_CAND_LDS       the 8 candidate planes staged in LDS (k_sweep)
+//   ACMMP_COMPACT_REFINE refinement items packed across lanes (refine_costs_compact)
+//   ACMMP_PIPE_ROWS      software-pipelined patch rows (ncc_sums_rows)
 #ifndef ACMMP_WAVE2D
 #define ACMMP_WAVE2D 4
 #endif
 #ifndef ACMMP_CAND_LDS
 #define ACMMP_CAND_LDS 1
 #endif
+#ifndef ACMMP_COMPACT_REFINE
+#define ACMMP_COMPACT_REFINE 1
+#endif
+#if ACMMP_COMPACT_REFINE && !ACMMP_CAND_LDS
+#error "ACMMP_COMPACT_REFINE works in the LDS candidate slots (ACMMP_CAND_LDS=1)"
+#endif
 #ifndef ACMMP_PIPE_ROWS
 #define ACMMP_PIPE_ROWS 1
 #endif
+// Minimum waves per SIMD the sweep kernel is register-allocated for
+// (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
 #ifndef ACMMP_SWEEP_WAVES
 #define ACMMP_SWEEP_WAVES 2
 #endif
@@ -904,16 +916,15 @@ DEV BlockXY xcd_block() {
 // x R rows of the block instead of one 64-column row, so its gathers for
 // neighbouring patch rows overlap in the source image (L1 reuse within a
 // wave); the lane -> pixel map is all that changes.
-DEV LaneGeom lane_geom(int colour, BlockXY b) {
+DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     LaneGeom g;
 #if ACMMP_WAVE2D > 1
     static_assert(kBX == 64 && kBY == 4 && (ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4), "2D wave map of 64x4 blocks");
     constexpr int R = ACMMP_WAVE2D, C = 64 / R;
-    const int tid = threadIdx.y * kBX + threadIdx.x;
     const int w = tid >> 6, l = tid & 63;
     const int tx = (w % R) * C + (l % C), ty = (w / R) * R + l / C;
 #else
-    const int tx = threadIdx.x, ty = threadIdx.y;
+    const int tx = tid % kBX, ty = tid / kBX;
 #endif
     g.k = b.bx * kBX + tx;
     g.py = b.by * kBY + ty;
@@ -922,6 +933,8 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) {
     g.tb = ty * kTileW + tx + g.s;
     return g;
 }
+
+DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, threadIdx.y * kBX + threadIdx.x); }
 
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
@@ -1011,6 +1024,99 @@ struct ViewCounts {
     }
     __device__ __forceinline__ int get(int j) const { return (int)(((j < 16) ? (lo >> (4 * j)) : (hi >> (4 * (j - 16)))) & 15u); }
 };
+
+// ------------------------------------------------- compacted refinement
+// The candidate-plane slots (cand_lds: 8 float4 per lane, slot d of lane i at
+// [d * kThreads + i]) are dead after the t = 0 accept and are reused, each
+// lane only within its OWN 8 slots (waves progress independently, so a
+// lane's slots may still hold live candidates of another wave's t = 0 step
+// — nothing may spill across lanes of different waves):
+//   slots 0..4 = the 5 refinement planes; slot 5 = results of planes 0..3;
+//   slot 6 = (result of plane 4, mean, var, inv_wsum); slot 7.x = the wave's
+//   owner list entry of this lane's rank.
+DEV float &cmp_res(float4 *lds, int t, int lane) {
+    return reinterpret_cast<float *>(lds)[4 * ((5 + (t >> 2)) * kThreads + lane) + (t & 3)];
+}
+DEV float &cmp_pd(float4 *lds, int k, int lane) {  // k = 1 mean, 2 var, 3 inv_wsum
+    return reinterpret_cast<float *>(lds)[4 * (6 * kThreads + lane) + k];
+}
+DEV int &cmp_list(float4 *lds, int lane) { return reinterpret_cast<int *>(lds)[4 * (7 * kThreads + lane)]; }
+
+DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The 5 refinement hypotheses of PlaneHypothesisRefinement (src/ACMMP.cu:
+// 743-783) cost sum_j w_j * (NCC_j (+ 0.2 geom_j)) over the lane's sampled
+// views j. Their planes are fixed before any of them is evaluated, so all 5
+// sums are formed here, view-major, and the sequential accept of the caller
+// then consumes them in order t = 1..5 (same operations, same order per
+// (lane, t): j ascending). Instead of one pass per (t, view with any lane
+// sampling it), the wave packs the (owner lane, t) items of view j into
+// ceil(5 c_j / active lanes) passes, c_j = lanes that sampled j: a lane
+// evaluates another lane's item with that lane's pixel, LDS patch weights,
+// tile offset and plane, and returns the cost through LDS. The view stays
+// wave-uniform (scalar SRD and cameras). Result: cmp_res(t, lane) = sum_t.
+template <int TX>
+DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, float4 *lds, const PixPatch &pp,
+                              const ViewCounts &vw, int nsrc, int colour, BlockXY blk, const float *ref_depths,
+                              const float4 *ref_normals, int px, int py) {
+    const acmmp_camera &c0 = kv.cam[0];
+    const int tid = pp.wo;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        float4 h = ref_normals[t];
+        h.w = distance_to_origin(c0, px, py, ref_depths[t], h);
+        lds[t * kThreads + tid] = h;
+    }
+    cmp_pd(lds, 1, tid) = pp.mean;
+    cmp_pd(lds, 2, tid) = pp.var;
+    cmp_pd(lds, 3, tid) = pp.inv_wsum;
+    const int lane = tid & 63, wbase = tid & ~63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t act = __ballot(1);
+    const int nact = __popcll(act), arank = __popcll(act & lt);
+    float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    wave_sync();
+    for (int j = 0; j < nsrc; ++j) {
+        const float wj = (float)vw.get(j);
+        const uint64_t m = __ballot(wj > 0);
+        if (m == 0) continue;
+        const int c = __popcll(m);
+        if (wj > 0) cmp_list(lds, wbase + __popcll(m & lt)) = lane;
+        wave_sync();
+        const int n = 5 * c;
+        for (int base = 0; base < n; base += nact) {
+            const int k = base + arank;
+            if (k < n) {
+                const int t = k / c;
+                const int otid = wbase + cmp_list(lds, wbase + (k - t * c));
+                const LaneGeom og = lane_geom_of(colour, blk, otid);
+                PixPatch op;
+                op.wo = otid;
+                op.w = wlds + otid;
+                op.rt = tile + og.tb;
+                op.mean = cmp_pd(lds, 1, otid);
+                op.var = cmp_pd(lds, 2, otid);
+                op.inv_wsum = cmp_pd(lds, 3, otid);
+                const float4 h = lds[t * kThreads + otid];
+                const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, j + 1, og.px, og.py, h);
+                cmp_res(lds, t, otid) = kv.prm.geom_consistency ? cc + 0.2f * geom_cost(kv, j + 1, h, og.px, og.py) : cc;
+            }
+        }
+        wave_sync();
+        if (wj > 0) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t) acc[t] += wj * cmp_res(lds, t, tid);
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int t = 0; t < 5; ++t) cmp_res(lds, t, tid) = acc[t];
+    wave_sync();
+}
 
 // ------------------------------------------------------------- the sweep
 // CheckerboardPropagation (src/ACMMP.cu:786-1173) for the pixels of one colour.
@@ -1382,6 +1488,14 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         // views with a zero sampled weight contribute +0 in the reference
         // (weight 0 * finite cost), so their NCC is skipped: bit-identical
         float tc = 0.0f;
+#if ACMMP_COMPACT_REFINE
+        if (t >= 1) {
+            if (t == 1)
+                refine_costs_compact<TX>(kv, tile, wlds, cand_lds, pp, vw, nsrc, colour, blk, ref_depths,
+                                         ref_normals, px, py);
+            tc = cmp_res(cand_lds, t - 1, pp.wo);
+        } else
+#endif
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
