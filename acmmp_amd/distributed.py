@@ -146,7 +146,8 @@ class ViewParallelPipeline:
     def __init__(self, dense_folder: str, output_dir: str = "/ACMMP", device: int = 0, seed: int = 1234,
                  max_iterations: int = 0, geom_iterations: int = 2, group=None,
                  compute: Optional[Callable] = None, jbu: Optional[Callable] = None, write_outputs: bool = True,
-                 comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None):
+                 comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None,
+                 concurrent_views: int = 1):
         self.dense = dense_folder
         self.output_folder = dense_folder + output_dir
         self.device = device
@@ -159,6 +160,10 @@ class ViewParallelPipeline:
         self.compute = compute or engine_compute(device)
         self.jbu = jbu or gpu_jbu(device)
         self.write_outputs = write_outputs
+        # views of a pass computed at once (each on its own engine / HIP stream,
+        # from a thread: ctypes drops the GIL in every library call), so one
+        # view's launches fill the tail of another's and host copies overlap
+        self.concurrent_views = max(int(concurrent_views), 1)
         if tensor_device is None:
             tensor_device = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
         self.tdev = tensor_device
@@ -228,6 +233,7 @@ class ViewParallelPipeline:
     # --------------------------------------------------------------- pass
     def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
         local = {}
+        tasks = []
         for v in self.mine:
             p = self.problems[v]
             ids = [p.ref_image_id] + p.sources
@@ -248,11 +254,19 @@ class ViewParallelPipeline:
                 w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
                 scaled = np.concatenate([prev.planes[..., :3], w[..., None]], -1).astype(np.float32)
                 t.hier_inputs = (scaled, up)
-            res = self.compute(t)
+            tasks.append(t)
+        if self.concurrent_views > 1 and len(tasks) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=self.concurrent_views) as ex:
+                results = list(ex.map(self.compute, tasks))
+        else:
+            results = [self.compute(t) for t in tasks]
+        for t, res in zip(tasks, results):  # in view order, as the sequential loop
+            v = t.index
             self.state[v] = res
             local[v] = torch.from_numpy(np.ascontiguousarray(res.planes[..., 3]))
             if self.write_outputs:
-                self._write(p.ref_image_id, res, geom)
+                self._write(t.ref_id, res, geom)
         self.depths = exchange.gather(self.rank, local)
         self.pass_index += 1
 
@@ -300,6 +314,8 @@ def main():
     ap.add_argument("--iterations", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--backend", default=None, help="nccl (RCCL, default with GPUs) or gloo")
+    ap.add_argument("--concurrent_views", type=int, default=2,
+                    help="views computed at once per GPU (one engine / HIP stream each)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -309,7 +325,7 @@ def main():
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend)
     pipe = ViewParallelPipeline(args.dense_folder, args.output_dir, device=local_rank, seed=args.seed,
-                                max_iterations=args.iterations)
+                                max_iterations=args.iterations, concurrent_views=args.concurrent_views)
     out = pipe.run()
     if pipe.rank == 0:
         print(f"Depth/normal/cost maps written under {out}")

@@ -50,8 +50,11 @@ def jacobi_maps(dense):
     return OraclePipeline(dense).run_single_scale("jacobi")
 
 
-def test_world1_matches_oracle_jacobi(dense, jacobi_maps):
-    out = ViewParallelPipeline(dense, "/VP1", device=0).run()
+@pytest.mark.parametrize("concurrent", [1, 2])
+def test_world1_matches_oracle_jacobi(dense, jacobi_maps, concurrent):
+    """World size 1; concurrent=2 computes two views at once on two engines
+    (HIP streams) from two threads — the outputs must not change."""
+    out = ViewParallelPipeline(dense, f"/VP1c{concurrent}", device=0, concurrent_views=concurrent).run()
     assert _compare(out, jacobi_maps) == 5 * 4
 
 
