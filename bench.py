@@ -25,6 +25,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -139,22 +140,49 @@ def main():
         if not geom:
             eng.export_results(planes[k].data_ptr(), costs[k].data_ptr(), my_depth[k].data_ptr())
 
+    stats_lock = threading.Lock()
+
     def finish_view(eng, geom: bool):
         eng.synchronize()
         t = eng.timing()
-        st = sweep_stats["geom" if geom else "photo"]
-        st[0] += t["sweep_ms"]
-        st[1] += t["sweep_launches"]
+        with stats_lock:
+            st = sweep_stats["geom" if geom else "photo"]
+            st[0] += t["sweep_ms"]
+            st[1] += t["sweep_launches"]
 
     def run_pass(geom: bool):
-        S = len(engines)
+        # one host thread per engine takes the next view off a shared queue as
+        # soon as its own previous view finished (no lockstep rounds, so a view
+        # that ends early does not leave the GPU to its partner's tail); the
+        # library calls release the GIL (ctypes)
         work = list(enumerate(mine))
-        for r in range(0, len(work), S):
-            batch = list(zip(engines, work[r:r + S]))
-            for eng, (k, v) in batch:
-                launch_view(eng, k, v, geom)
-            for eng, _ in batch:
-                finish_view(eng, geom)
+        if len(engines) == 1:
+            for k, v in work:
+                launch_view(engines[0], k, v, geom)
+                finish_view(engines[0], geom)
+            return
+        errors = []
+
+        def worker(eng):
+            try:
+                while True:
+                    with stats_lock:
+                        if not work or errors:
+                            return
+                        k, v = work.pop(0)
+                    launch_view(eng, k, v, geom)
+                    finish_view(eng, geom)
+            except BaseException as e:  # re-raised on the main thread
+                with stats_lock:
+                    errors.append(e)
+
+        threads = [threading.Thread(target=worker, args=(e,)) for e in engines]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
 
 
     def step():
