@@ -6,6 +6,13 @@
  * bench.py's cpu_baseline leg may load it; the product (acmmp_amd/) never
  * links, calls or falls back to it.
  *
+ * PARITY UNPINNED against reference outputs: the reference engine cannot be
+ * built here (nvcc/CUDA, cuRAND, OpenCV, Boost absent) and seeds its RNG from
+ * clock64(), and no reference test or fixture holds PatchMatch outputs. The
+ * restatement is pinned by analytic known-answer tests, the Random123
+ * Philox4x32-10 vectors and fixtures the reference's own colmap2mvsnet_acm.py
+ * produced (tests/test_oracle_kat.py, tests/golden/).
+ *
  * What it restates (line by line, one C function per reference function):
  *   rlav440/ACMMP src/ACMMP.cu:24-1352 (device code) and :1378-1456 (RunPatchMatch).
  * With the pinned semantics of SURVEY.md Appendix A:

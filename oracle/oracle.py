@@ -4,6 +4,8 @@ TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
 bench.py's cpu_baseline leg — never by the product package acmmp_amd/.
 The oracle restates src/ACMMP.cu (rlav440/ACMMP) on the CPU with the pinned
 semantics of SURVEY.md Appendix A; see the header of acmmp_oracle.c.
+Parity unpinned against reference outputs (unbuildable here, clock64()-seeded):
+pinned by known-answer tests, Philox vectors and the colmap fixtures only.
 """
 from __future__ import annotations
 
