@@ -47,6 +47,9 @@ struct Huff {
     // canonical decoding tables: maxcode[l], valptr[l], mincode[l]
     int32_t mincode[17], maxcode[18], valptr[17];
     uint8_t vals[256];
+    // 8-bit lookahead: for the next 8 bits of the stream, the length (0 = the
+    // code is longer than 8 bits) and symbol of the code they start with
+    uint8_t look_len[256], look_sym[256];
     bool present = false;
 };
 
@@ -95,6 +98,21 @@ bool build_huff(Huff &h, const uint8_t *counts, const uint8_t *symbols, int nsym
         code <<= 1;
     }
     h.maxcode[17] = 0x7fffffff;
+    std::memset(h.look_len, 0, sizeof(h.look_len));
+    for (int l = 1; l <= 8; ++l) {
+        // empty when maxcode[l] == -1; a code that overflows l bits, or an
+        // entry a shorter code already holds, is left to the bit-serial loop
+        // (which takes the shortest match, as libjpeg does)
+        for (int c = h.mincode[l]; c <= h.maxcode[l] && c < (1 << l); ++c) {
+            const int sym = h.vals[h.valptr[l] + c - h.mincode[l]];
+            const int span = 1 << (8 - l);
+            for (int e = c << (8 - l), k = 0; k < span; ++k) {
+                if (h.look_len[e + k]) continue;
+                h.look_len[e + k] = (uint8_t)l;
+                h.look_sym[e + k] = (uint8_t)sym;
+            }
+        }
+    }
     h.present = true;
     return true;
 }
@@ -133,6 +151,12 @@ inline int getbits(Jpeg &j, int n) {
 
 inline int decode_huff(Jpeg &j, const Huff &h) {
     fill(j);
+    const int peek = (int)(j.bitbuf >> 24);
+    if (const int len = h.look_len[peek]) {  // codes of up to 8 bits: one lookup
+        j.bitbuf <<= len;
+        j.bitcnt -= len;
+        return h.look_sym[peek];
+    }
     int code = 0;
     for (int l = 1; l <= 16; ++l) {
         code = (code << 1) | (int)(j.bitbuf >> 31);

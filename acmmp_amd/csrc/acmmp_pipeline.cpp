@@ -16,12 +16,14 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/acmmp.hpp"
@@ -176,6 +178,34 @@ int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
 
 // One view of InputInitialization (src/ACMMP.cpp:536-598): image + camera,
 // camera size from the image, rescaled to max_image_size when larger.
+// Runs fn(0..n-1) on up to 16 host threads. Returns the status of the lowest
+// failing index and leaves its message in this thread's error slot, so the
+// caller sees what the sequential loop would have reported first.
+template <class Fn>
+int parallel_views(int n, Fn fn) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int workers = std::min<int>(n, (int)std::min(hw, 16u));
+    std::vector<int> rc((size_t)n, ACMMP_OK);
+    std::vector<std::string> msg((size_t)n);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            rc[(size_t)i] = fn(i);
+            if (rc[(size_t)i]) msg[(size_t)i] = g_err;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < workers; ++t) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rc[(size_t)i]) {
+            g_err = msg[(size_t)i];
+            return rc[(size_t)i];
+        }
+    return ACMMP_OK;
+}
+
 int load_view(const std::string &dense, int id, int max_image_size, acmmp::Image &im, acmmp_camera &cam) {
     int rc = load_image(image_path(dense, id), im);
     if (rc) return rc;
@@ -380,33 +410,40 @@ int acmmp_input_initialization(acmmp_ctx *ctx, const char *dense_folder, const c
     std::vector<acmmp_camera> cams((size_t)n);
     // a source view uses the cur_image_size of the problem indexed by its
     // image id, as the reference does (src/ACMMP.cpp:564-568)
-    for (int i = 0; i < n; ++i) {
-        const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
-        if (i > 0 && (id < 0 || id >= count))
+    for (int i = 1; i < n; ++i) {
+        const int id = pr.src_image_ids[i - 1];
+        if (id < 0 || id >= count)
             return fail(ACMMP_ERR_ARG, "source id %d is not a problem index (pair.txt ids must be 0..n-1)", id);
-        const int max_image_size = i == 0 ? pr.cur_image_size : problems[id].cur_image_size;
-        const int rc = load_view(dense, id, max_image_size, images[(size_t)i], cams[(size_t)i]);
-        if (rc) return rc;
     }
+    // the n decodes (+ resizes) are independent: host threads, results and
+    // the first error in view order identical to the sequential loop
+    int rc = parallel_views(n, [&](int i) {
+        const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
+        const int max_image_size = i == 0 ? pr.cur_image_size : problems[id].cur_image_size;
+        return load_view(dense, id, max_image_size, images[(size_t)i], cams[(size_t)i]);
+    });
+    if (rc) return rc;
     std::vector<const float *> ptrs((size_t)n);
     for (int i = 0; i < n; ++i) ptrs[(size_t)i] = images[(size_t)i].data.data();
-    int rc = acmmp_set_images(ctx, n, cams.data(), ptrs.data(), 0);  // depth range x0.6 / x1.2 (:600-605)
+    rc = acmmp_set_images(ctx, n, cams.data(), ptrs.data(), 0);  // depth range x0.6 / x1.2 (:600-605)
     if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
     acmmp_params p;
     acmmp_get_params(ctx, &p);
     if (p.geom_consistency) {  // :608-635
         const std::string suffix = p.multi_geometry ? "/depths_geom.dmb" : "/depths.dmb";
         std::vector<std::vector<float>> depths((size_t)n);
-        for (int i = 0; i < n; ++i) {
+        rc = parallel_views(n, [&](int i) {
             const int id = i == 0 ? pr.ref_image_id : pr.src_image_ids[i - 1];
             int h = 0, w = 0, nb = 0;
-            rc = read_dmb(result_folder(output_folder, id) + suffix, depths[(size_t)i], h, w, nb);
-            if (rc) return rc;
+            const int r = read_dmb(result_folder(output_folder, id) + suffix, depths[(size_t)i], h, w, nb);
+            if (r) return r;
             if (nb != 1 || h != cams[(size_t)i].height || w != cams[(size_t)i].width)
                 return fail(ACMMP_ERR_IO, "depth map of view %d is %dx%dx%d, image is %dx%d", id, w, h, nb,
                             cams[(size_t)i].width, cams[(size_t)i].height);
-            ptrs[(size_t)i] = depths[(size_t)i].data();
-        }
+            return (int)ACMMP_OK;
+        });
+        if (rc) return rc;
+        for (int i = 0; i < n; ++i) ptrs[(size_t)i] = depths[(size_t)i].data();
         rc = acmmp_set_depth_maps(ctx, ptrs.data());
         if (rc) return fail(rc, "%s", acmmp_last_error(ctx));
     }

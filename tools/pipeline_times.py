@@ -1,0 +1,81 @@
+"""End-to-end timing of the pass driver on BASELINE cfg4's shape on ONE GPU.
+
+cfg4 (BASELINE.json configs[3]): 49 views at 1600x1200, each with its 20 best
+source views (N = 21, colmap2mvsnet_acm.py:415), main_ACMMP's multi-scale loop
+(src/main_ACMMP.cpp:96-176: planar-prior pass, geometric passes, JBU +
+hierarchy on the finer scale). The reference runs it on 8 GPUs; here the
+same folder runs on one GPU through
+
+  distributed   acmmp_amd.distributed.ViewParallelPipeline (world 1, Jacobi
+                order, 2 views in flight on 2 HIP streams)
+  cli           acmmp_amd/lib/acmmp_main --no_fusion (the C++ driver,
+                sequential Gauss-Seidel order, one engine)
+  fusion        RunFusion over the CLI's maps (C++, host)
+
+Synthetic, seeded scene rendered on the GPU and written as 8-bit JPEGs (a
+COLMAP-converted dense folder); wall times include JPEG decode and .dmb I/O,
+as the reference's do. Iterations: the driver's default (the reference's).
+usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] > gpurun_out/pipeline.jsonl
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from acmmp_amd import scene  # noqa: E402
+from acmmp_amd import pipeline  # noqa: E402
+from acmmp_amd.distributed import ViewParallelPipeline  # noqa: E402
+
+V = int(sys.argv[1]) if len(sys.argv) > 1 else 49
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 1600
+H = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
+NSRC = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    setup = scene.scene_setup(num_views=V, width=W, height=H)
+    views = []
+    for i in range(V):
+        img = scene.render_torch(setup, i, dev).cpu().numpy()
+        R, t, _, _ = setup.poses[i]
+        views.append(scene.View(K=setup.K.astype(np.float32), R=R.astype(np.float32), t=t.astype(np.float32),
+                                image=img, depth=None, normal=None))
+    sc = scene.Scene(views=views, pairs=setup.pairs)
+    tmp = tempfile.mkdtemp(prefix="acmmp_cfg4_")
+    dense = os.path.join(tmp, "dense")
+    t0 = time.perf_counter()
+    scene.write_dense_folder(sc, dense, num_src=NSRC)
+    emit(step="write_dense", views=V, width=W, height=H, nsrc=NSRC, s=round(time.perf_counter() - t0, 2))
+
+    t0 = time.perf_counter()
+    ViewParallelPipeline(dense, "/ACMMP_dist", device=0, concurrent_views=2).run()
+    torch.cuda.synchronize()
+    emit(step="distributed_world1", order="jacobi", concurrent_views=2, s=round(time.perf_counter() - t0, 2))
+    shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
+
+    cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
+    t0 = time.perf_counter()
+    subprocess.run([cli, dense, "--output_dir", "/ACMMP", "--no_fusion"], stdout=sys.stderr, check=True)
+    emit(step="cli", order="sequential", s=round(time.perf_counter() - t0, 2))
+
+    t0 = time.perf_counter()
+    n = pipeline.run_fusion(dense, dense + "/ACMMP")
+    emit(step="fusion", points=n, s=round(time.perf_counter() - t0, 2))
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
