@@ -15,6 +15,8 @@
 // unpinned).
 #include <sys/stat.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -22,6 +24,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/acmmp.h"
@@ -84,6 +87,32 @@ float get_angle(const float *a, const float *b) {  // GetAngle
     const float angle = std::acos(dot);
     if (angle != angle) return 0.0f;
     return angle;
+}
+
+// Runs fn(0..n-1) on up to 16 host threads; returns the status of the lowest
+// failing index with its message (what the sequential loop reports first).
+template <class Fn>
+int parallel_for(int n, Fn fn) {
+    const int workers = std::min<int>(n, (int)std::min(std::max(1u, std::thread::hardware_concurrency()), 16u));
+    std::vector<int> rc((size_t)std::max(n, 0), ACMMP_OK);
+    std::vector<std::string> msg(rc.size());
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            rc[(size_t)i] = fn(i);
+            if (rc[(size_t)i]) msg[(size_t)i] = f_err;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < workers; ++t) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rc[(size_t)i]) {
+            f_err = msg[(size_t)i];
+            return rc[(size_t)i];
+        }
+    return ACMMP_OK;
 }
 
 int read_dmb(const std::string &path, std::vector<float> &d, int &h, int &w, int &nb) {
@@ -259,9 +288,11 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     std::vector<std::vector<float>> depths(n), normals(n);
     std::vector<int> rows(n), cols(n);
     std::map<int, int> image_id_2_index;
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < n; ++i) image_id_2_index[problems[i].ref_image_id] = (int)i;
+    // views load independently (JPEG decode, two .dmb reads, optional mask)
+    int load_rc = parallel_for((int)n, [&](int vi) -> int {
+        const size_t i = (size_t)vi;
         const int id = problems[i].ref_image_id;
-        image_id_2_index[id] = (int)i;
         const std::string ipath = image_folder + "/" + id8(id) + ".jpg";
         int iw = 0, ih = 0;
         std::vector<uint8_t> img;
@@ -311,7 +342,9 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             resize_u8(m8, mw, mh, 1, mr, w, h);
             for (size_t k = 0; k < mr.size(); ++k) masks[i][k] = mr[k] < 128 ? 1 : 0;
         }
-    }
+        return (int)ACMMP_OK;
+    });
+    if (load_rc) return load_rc;
 
     std::vector<Point> cloud;
     for (size_t i = 0; i < n; ++i) {
@@ -328,59 +361,102 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                              problems[i].ref_image_id);
             src_index[j] = it->second;
         }
-        for (int r = 0; r < H; ++r) {
-            for (int c = 0; c < W; ++c) {
-                const size_t pc = (size_t)r * W + c;
-                if (masks[i][pc] == 1) continue;
-                const float ref_depth = depths[i][pc];
-                const float *ref_normal = &normals[i][pc * 3];
-                if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
-                const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
-                const uint8_t *bgr = &images[i][pc * 3];
-                int num_consistent = 0;
-                float dynamic_consistency = 0;
-                for (int j = 0; j < num_ngb; ++j) {
-                    const int s = src_index[j];
-                    const int src_cols = cols[s], src_rows = rows[s];
-                    float ptx, pty, proj_depth;
-                    project(PointX, cameras[s], ptx, pty, proj_depth);
-                    const int src_r = int(pty + 0.5f);
-                    const int src_c = int(ptx + 0.5f);
-                    if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
-                        const size_t sp = (size_t)src_r * src_cols + src_c;
-                        if (masks[s][sp] == 1) continue;
-                        const float src_depth = depths[s][sp];
-                        const float *src_normal = &normals[s][sp * 3];
-                        if (src_depth <= 0.0) continue;
-                        const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
-                        float tx, ty;
-                        project(tmp_X, cameras[i], tx, ty, proj_depth);
-                        const float reproj_error = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
-                        const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
-                        const float angle = get_angle(ref_normal, src_normal);
-                        if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
-                            used_x[j] = src_c;
-                            used_y[j] = src_r;
-                            const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                            dynamic_consistency += std::exp(-tmp_index);
-                            num_consistent++;
+        // Two phases per band of rows, exact to the sequential loop: (1) on
+        // host threads, every pixel's per-source projections and consistency
+        // tests against the masks as they stand (masks only ever go 0 -> 1,
+        // so a source masked now stays masked); (2) in the reference's pixel
+        // order, the sources that passed are re-checked against the current
+        // masks and accumulated in ascending j (same exp values, same sum
+        // order), then points are emitted and masks / used_list updated.
+        struct Hit {
+            int j;
+            uint32_t sp;
+            float ex;
+        };
+        const int band = 32;
+        const int ngb = std::max(num_ngb, 1);
+        std::vector<uint8_t> live((size_t)band * W);
+        std::vector<uint8_t> nhit((size_t)band * W);
+        std::vector<Hit> hits((size_t)band * W * ngb);
+        for (int r0 = 0; r0 < H; r0 += band) {
+            const int r1 = std::min(H, r0 + band);
+            parallel_for(r1 - r0, [&](int rr) -> int {
+                const int r = r0 + rr;
+                for (int c = 0; c < W; ++c) {
+                    const size_t pc = (size_t)r * W + c, q = (size_t)rr * W + c;
+                    live[q] = 0;
+                    nhit[q] = 0;
+                    if (masks[i][pc] == 1) continue;
+                    const float ref_depth = depths[i][pc];
+                    const float *ref_normal = &normals[i][pc * 3];
+                    if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
+                    live[q] = 1;
+                    const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
+                    Hit *h = &hits[q * ngb];
+                    int k = 0;
+                    for (int j = 0; j < num_ngb; ++j) {
+                        const int s = src_index[j];
+                        const int src_cols = cols[s], src_rows = rows[s];
+                        float ptx, pty, proj_depth;
+                        project(PointX, cameras[s], ptx, pty, proj_depth);
+                        const int src_r = int(pty + 0.5f);
+                        const int src_c = int(ptx + 0.5f);
+                        if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
+                            const size_t sp = (size_t)src_r * src_cols + src_c;
+                            if (masks[s][sp] == 1) continue;
+                            const float src_depth = depths[s][sp];
+                            const float *src_normal = &normals[s][sp * 3];
+                            if (src_depth <= 0.0) continue;
+                            const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
+                            float tx, ty;
+                            project(tmp_X, cameras[i], tx, ty, proj_depth);
+                            const float reproj_error = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
+                            const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
+                            const float angle = get_angle(ref_normal, src_normal);
+                            if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
+                                const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
+                                h[k++] = Hit{j, (uint32_t)sp, std::exp(-tmp_index)};
+                            }
                         }
                     }
+                    nhit[q] = (uint8_t)k;
                 }
-                if (num_consistent >= con_num_thresh &&
-                    (dynamic_consistency > consistency_scalar * num_consistent)) {
-                    Point p;
-                    p.coord = PointX;
-                    p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
-                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
-                    cloud.push_back(p);
-                    // used_list is not reset per pixel in the reference: stale entries apply too
-                    for (int j = 0; j < num_ngb; ++j) {
-                        if (used_x[j] == -1) continue;
-                        const int s = src_index[j];
-                        masks[s][(size_t)used_y[j] * cols[s] + used_x[j]] = 1;
-                        // `approved` is this view's W x H image indexed by source coordinates (:1030)
-                        if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
+                return (int)ACMMP_OK;
+            });
+            for (int r = r0; r < r1; ++r) {
+                for (int c = 0; c < W; ++c) {
+                    const size_t pc = (size_t)r * W + c, q = (size_t)(r - r0) * W + c;
+                    // masks[i] changes during view i only if i is its own source
+                    if (!live[q] || masks[i][pc] == 1) continue;
+                    int num_consistent = 0;
+                    float dynamic_consistency = 0;
+                    const Hit *h = &hits[q * ngb];
+                    for (int k = 0; k < nhit[q]; ++k) {
+                        const int s = src_index[h[k].j];
+                        if (masks[s][h[k].sp] == 1) continue;
+                        used_x[h[k].j] = (int)(h[k].sp % (uint32_t)cols[s]);
+                        used_y[h[k].j] = (int)(h[k].sp / (uint32_t)cols[s]);
+                        dynamic_consistency += h[k].ex;
+                        num_consistent++;
+                    }
+                    if (num_consistent >= con_num_thresh &&
+                        (dynamic_consistency > consistency_scalar * num_consistent)) {
+                        const float ref_depth = depths[i][pc];
+                        const float *ref_normal = &normals[i][pc * 3];
+                        const uint8_t *bgr = &images[i][pc * 3];
+                        Point p;
+                        p.coord = world_point(c, r, ref_depth, cameras[i]);
+                        p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
+                        p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
+                        cloud.push_back(p);
+                        // used_list is not reset per pixel in the reference: stale entries apply too
+                        for (int j = 0; j < num_ngb; ++j) {
+                            if (used_x[j] == -1) continue;
+                            const int s = src_index[j];
+                            masks[s][(size_t)used_y[j] * cols[s] + used_x[j]] = 1;
+                            // `approved` is this view's W x H image indexed by source coordinates (:1030)
+                            if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
+                        }
                     }
                 }
             }
