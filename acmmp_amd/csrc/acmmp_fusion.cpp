@@ -5,8 +5,11 @@
 //
 // Host code, literal: the reference's fusion is order-dependent (a pixel's
 // approval masks pixels of other views that later pixels then skip, and
-// used_list is never reset between pixels), so it runs sequentially in the
-// reference's order with the reference's float expression order
+// used_list is never reset between pixels), so approvals run sequentially in
+// the reference's order with the reference's float expression order; the
+// per-pixel projections and tests before them run on host threads per band
+// of rows and are re-checked against the masks at approval time (exact: masks
+// only ever go 0 -> 1)
 // (Get3DPointonWorld / ProjectonCamera src/ACMMP.cpp:203-251, GetAngle
 // :253-262). Deviations: no cv::imshow (:897-900); the PLY is written in
 // point order (the reference's OpenMP-critical writes make its order
@@ -534,7 +537,15 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         masks[i].assign((size_t)w * h, 0);
     }
     std::vector<Point> cloud;
-    std::vector<CInfo> cand0, cand1;
+    // Same two-phase scheme as RunFusion: candidates (projection + metrics of
+    // both maps) per band of rows on host threads against the current masks,
+    // then the reference's pixel order with every approval re-checked
+    // against the masks as they stand then (they only ever go 0 -> 1).
+    struct Ok {  // a below-threshold candidate: the only kind that counts or masks
+        int im, x, y;
+        float dc;
+    };
+    const int band = 32;
     for (size_t i = 0; i < n; ++i) {
         const int W = in.cols[i], H = in.rows[i];
         std::vector<int> srcs;
@@ -543,71 +554,89 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
             if (it == image_id_2_index.end()) return ffail(ACMMP_ERR_ARG, "source is not a problem");
             srcs.push_back(it->second);
         }
-        for (int r = 0; r < H; ++r) {
-            for (int c = 0; c < W; ++c) {
-                const size_t pc = (size_t)r * W + c;
-                if (masks[i][pc] == 1) continue;
-                const float ref_depth = in.depths[i][pc], ref_p_depth = in.pdepths[i][pc];
-                const float *ref_normal = &in.normals[i][pc * 3], *ref_p_normal = &in.pnormals[i][pc * 3];
-                if (ref_depth <= 0.0 && ref_p_depth <= 0.0) continue;
-                float d_cons_0 = 0, d_cons_1 = 0;
-                int n0 = 0, n1 = 0;
-                bool t0 = false, t1 = false;
-                cand0.clear();
-                cand1.clear();
-                if (ref_depth > 0.0) {
-                    candidates(in, masks, srcs, i, r, c, ref_depth, ref_normal, cand0);
-                    for (const CInfo &k : cand0)
-                        if (k.below_thresh) {
-                            n0++;
-                            d_cons_0 += k.dynamic_consistency;
-                        }
-                    t0 = (n0 >= num_consistent_thresh) && (d_cons_0 > consistency_scalar * n0);
-                }
-                if (ref_p_depth > 0.0) {
-                    candidates(in, masks, srcs, i, r, c, ref_p_depth, ref_p_normal, cand1);
-                    for (const CInfo &k : cand1)
-                        if (k.below_thresh) {
-                            n1++;
-                            d_cons_1 += k.dynamic_consistency;
-                        }
-                    t1 = (n1 >= num_consistent_thresh) && (d_cons_1 > consistency_scalar * n1);
-                }
-                const std::vector<CInfo> *iter = nullptr;
-                bool passing = false;
-                float g_depth = 0;
-                const float *g_normal = ref_normal;
-                if (t0 && t1) {  // (:754-769)
-                    passing = true;
-                    if (n1 >= n0) {
-                        iter = &cand1;
-                        g_depth = ref_p_depth;
-                        g_normal = ref_p_normal;
-                    } else {
-                        iter = &cand0;
-                        g_depth = ref_depth;
-                        g_normal = ref_normal;
+        const int ns = std::max((int)srcs.size(), 1);
+        // per pixel: bit 0 live, bit 1 map 0 evaluated, bit 2 map 1 evaluated
+        std::vector<uint8_t> state((size_t)band * W);
+        std::vector<uint8_t> cnt((size_t)band * W * 2);
+        std::vector<Ok> oks((size_t)band * W * 2 * ns);
+        for (int r0 = 0; r0 < H; r0 += band) {
+            const int r1 = std::min(H, r0 + band);
+            parallel_for(r1 - r0, [&](int rr) -> int {
+                const int r = r0 + rr;
+                std::vector<CInfo> cand;
+                for (int c = 0; c < W; ++c) {
+                    const size_t pc = (size_t)r * W + c, q = (size_t)rr * W + c;
+                    state[q] = 0;
+                    if (masks[i][pc] == 1) continue;
+                    const float ref_depth = in.depths[i][pc], ref_p_depth = in.pdepths[i][pc];
+                    if (ref_depth <= 0.0 && ref_p_depth <= 0.0) continue;
+                    uint8_t st = 1;
+                    for (int b = 0; b < 2; ++b) {
+                        const float d = b ? ref_p_depth : ref_depth;
+                        cnt[2 * q + b] = 0;
+                        if (!(d > 0.0)) continue;
+                        st |= (uint8_t)(2 << b);
+                        candidates(in, masks, srcs, i, r, c, d, b ? &in.pnormals[i][pc * 3] : &in.normals[i][pc * 3],
+                                   cand);
+                        Ok *o = &oks[(2 * q + b) * ns];
+                        int k = 0;
+                        for (const CInfo &ci : cand)
+                            if (ci.below_thresh) o[k++] = Ok{ci.im_num, ci.x, ci.y, ci.dynamic_consistency};
+                        cnt[2 * q + b] = (uint8_t)k;
                     }
-                } else if (t1) {
-                    passing = n1 >= (num_consistent_thresh + single_match_penalty);
-                    iter = &cand1;
-                    g_depth = ref_p_depth;
-                    g_normal = ref_p_normal;
-                } else {
-                    passing = t0 && n0 >= (num_consistent_thresh + single_match_penalty);
-                    iter = &cand0;
-                    g_depth = ref_depth;
-                    g_normal = ref_normal;
+                    state[q] = st;
                 }
-                if (passing) {
-                    Point p;
-                    p.coord = world_point(c, r, g_depth, in.cameras[i]);
-                    p.normal = F3{g_normal[0], g_normal[1], g_normal[2]};
-                    const uint8_t *bgr = &images[i][pc * 3];
-                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
-                    cloud.push_back(p);
-                    for (const CInfo &k : *iter)
-                        if (k.below_thresh) masks[k.im_num][(size_t)k.y * in.cols[k.im_num] + k.x] = 1;
+                return (int)ACMMP_OK;
+            });
+            for (int r = r0; r < r1; ++r) {
+                for (int c = 0; c < W; ++c) {
+                    const size_t pc = (size_t)r * W + c, q = (size_t)(r - r0) * W + c;
+                    if (!state[q] || masks[i][pc] == 1) continue;
+                    const float ref_depth = in.depths[i][pc], ref_p_depth = in.pdepths[i][pc];
+                    const float *ref_normal = &in.normals[i][pc * 3], *ref_p_normal = &in.pnormals[i][pc * 3];
+                    float d_cons[2] = {0, 0};
+                    int nb[2] = {0, 0};
+                    bool t[2] = {false, false};
+                    for (int b = 0; b < 2; ++b) {
+                        if (!(state[q] & (2 << b))) continue;
+                        Ok *o = &oks[(2 * q + b) * ns];
+                        int keep = 0;
+                        for (int k = 0; k < cnt[2 * q + b]; ++k) {
+                            if (masks[o[k].im][(size_t)o[k].y * in.cols[o[k].im] + o[k].x] == 1) continue;
+                            nb[b]++;
+                            d_cons[b] += o[k].dc;
+                            o[keep++] = o[k];
+                        }
+                        cnt[2 * q + b] = (uint8_t)keep;
+                        t[b] = (nb[b] >= num_consistent_thresh) && (d_cons[b] > consistency_scalar * nb[b]);
+                    }
+                    int pick = 0;
+                    bool passing = false;
+                    float g_depth = 0;
+                    const float *g_normal = ref_normal;
+                    if (t[0] && t[1]) {  // (:754-769)
+                        passing = true;
+                        pick = nb[1] >= nb[0] ? 1 : 0;
+                    } else if (t[1]) {
+                        passing = nb[1] >= (num_consistent_thresh + single_match_penalty);
+                        pick = 1;
+                    } else {
+                        passing = t[0] && nb[0] >= (num_consistent_thresh + single_match_penalty);
+                        pick = 0;
+                    }
+                    g_depth = pick ? ref_p_depth : ref_depth;
+                    g_normal = pick ? ref_p_normal : ref_normal;
+                    if (passing) {
+                        Point p;
+                        p.coord = world_point(c, r, g_depth, in.cameras[i]);
+                        p.normal = F3{g_normal[0], g_normal[1], g_normal[2]};
+                        const uint8_t *bgr = &images[i][pc * 3];
+                        p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
+                        cloud.push_back(p);
+                        const Ok *o = &oks[(2 * q + pick) * ns];
+                        for (int k = 0; k < cnt[2 * q + pick]; ++k)
+                            masks[o[k].im][(size_t)o[k].y * in.cols[o[k].im] + o[k].x] = 1;
+                    }
                 }
             }
         }
