@@ -164,6 +164,8 @@ class ViewParallelPipeline:
         # from a thread: ctypes drops the GIL in every library call), so one
         # view's launches fill the tail of another's and host copies overlap
         self.concurrent_views = max(int(concurrent_views), 1)
+        self._writer = None  # .dmb writer pool (created on the first write)
+        self._pending = []
         if tensor_device is None:
             tensor_device = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
         self.tdev = tensor_device
@@ -206,6 +208,8 @@ class ViewParallelPipeline:
         for i in sorted(need):
             if i not in self.index_of:
                 raise AcmmpError(f"source id {i} is not a problem index (pair.txt ids must be 0..n-1)")
+
+        def load(i):  # on a pool thread: the library call drops the GIL; its error slot is per thread
             size = self.problems[self.index_of[i]].cur_image_size
             cam = _abi.Camera()
             rc = lib.acmmp_load_view(self.dense.encode(), i, size, None, 0, C.byref(cam))
@@ -216,6 +220,13 @@ class ViewParallelPipeline:
                                      img.size, C.byref(cam))
             if rc != 0:
                 raise AcmmpError(f"acmmp_load_view({i}) failed: {lib.acmmp_pipeline_last_error().decode()}")
+            return img, cam
+
+        from concurrent.futures import ThreadPoolExecutor
+        order = sorted(need)
+        with ThreadPoolExecutor(max_workers=max(1, min(16, len(order)))) as ex:
+            loaded = list(ex.map(load, order))  # re-raises the first failure in id order
+        for i, (img, cam) in zip(order, loaded):
             self.images[i] = torch.from_numpy(img).to(self.tdev)
             self.cams[i] = cam
 
@@ -261,6 +272,7 @@ class ViewParallelPipeline:
                 results = list(ex.map(self.compute, tasks))
         else:
             results = [self.compute(t) for t in tasks]
+        self._flush_writes()  # the previous pass's files are complete before this pass rewrites them
         for t, res in zip(tasks, results):  # in view order, as the sequential loop
             v = t.index
             self.state[v] = res
@@ -271,11 +283,27 @@ class ViewParallelPipeline:
         self.pass_index += 1
 
     def _write(self, ref_id: int, res: ViewResult, geom: bool):
+        """Queues the view's three .dmb files on the writer pool: they are
+        outputs only (nothing in this driver reads them back), so they are
+        written while the next pass computes. A pass's writes start after the
+        previous pass's finished (the same files are rewritten every pass)."""
         folder = aio.result_folder(self.output_folder, ref_id)
         os.makedirs(folder, exist_ok=True)
-        aio.write_dmb(os.path.join(folder, "depths_geom.dmb" if geom else "depths.dmb"), res.planes[..., 3])
-        aio.write_dmb(os.path.join(folder, "normals.dmb"), res.planes[..., :3])
-        aio.write_dmb(os.path.join(folder, "costs.dmb"), res.costs)
+
+        def write():
+            aio.write_dmb(os.path.join(folder, "depths_geom.dmb" if geom else "depths.dmb"), res.planes[..., 3])
+            aio.write_dmb(os.path.join(folder, "normals.dmb"), res.planes[..., :3])
+            aio.write_dmb(os.path.join(folder, "costs.dmb"), res.costs)
+
+        if self._writer is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._writer = ThreadPoolExecutor(max_workers=4)
+        self._pending.append(self._writer.submit(write))
+
+    def _flush_writes(self):
+        pending, self._pending = self._pending, []
+        for f in pending:
+            f.result()  # re-raises a write error
 
     def run(self) -> str:
         os.makedirs(self.output_folder, exist_ok=True)
@@ -300,6 +328,10 @@ class ViewParallelPipeline:
             for g in range(self.geom_iterations):
                 self.run_pass(True, False, False, g > 0, exchange)
             max_down -= 1
+        self._flush_writes()
+        if self._writer is not None:
+            self._writer.shutdown()
+            self._writer = None
         if dist.is_initialized() and self.world > 1:
             dist.barrier(group=self.group)
         return self.output_folder
