@@ -20,8 +20,12 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <list>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -62,7 +66,62 @@ std::string image_path(const std::string &dense, int id) {
     return base + ".jpg";
 }
 
+// Decoded-image cache. The reference re-reads and re-decodes every image of a
+// problem in every pass (src/ACMMP.cpp:536-574: each view is decoded about
+// N times per pass); here a decode is kept, keyed by path and the file's
+// inode, size and mtime (so a rewritten file is decoded again), up to
+// ACMMP_IMAGE_CACHE_MB (default 4096, 0 disables) with LRU eviction.
+struct ImageCache {
+    struct Entry {
+        std::string key;
+        acmmp::Image im;
+    };
+    std::mutex mu;
+    std::list<Entry> lru;  // front = least recently used
+    std::map<std::string, std::list<Entry>::iterator> index;
+    size_t bytes = 0, cap = 0;
+    ImageCache() {
+        const char *e = std::getenv("ACMMP_IMAGE_CACHE_MB");
+        cap = (size_t)(e ? std::max(0L, std::atol(e)) : 4096L) << 20;
+    }
+    bool get(const std::string &key, acmmp::Image &out) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = index.find(key);
+        if (it == index.end()) return false;
+        lru.splice(lru.end(), lru, it->second);
+        out = it->second->im;
+        return true;
+    }
+    void put(const std::string &key, const acmmp::Image &im) {
+        const size_t b = im.data.size() * sizeof(float);
+        std::lock_guard<std::mutex> g(mu);
+        if (b > cap || index.count(key)) return;
+        while (bytes + b > cap && !lru.empty()) {
+            bytes -= lru.front().im.data.size() * sizeof(float);
+            index.erase(lru.front().key);
+            lru.pop_front();
+        }
+        lru.push_back(Entry{key, im});
+        index[key] = std::prev(lru.end());
+        bytes += b;
+    }
+};
+
+ImageCache &image_cache() {
+    static ImageCache c;
+    return c;
+}
+
 int load_image(const std::string &path, acmmp::Image &im) {
+    struct stat st;
+    std::string key;
+    if (::stat(path.c_str(), &st) == 0) {
+        char b[128];
+        std::snprintf(b, sizeof(b), "|%llu|%lld|%lld.%09ld", (unsigned long long)st.st_ino, (long long)st.st_size,
+                      (long long)st.st_mtim.tv_sec, (long)st.st_mtim.tv_nsec);
+        key = path + b;
+        if (image_cache().get(key, im)) return ACMMP_OK;
+    }
     int w = 0, h = 0;
     int rc = acmmp_image_size(path.c_str(), &w, &h);
     if (rc) return fail(rc, "cannot read image %s", path.c_str());
@@ -71,6 +130,7 @@ int load_image(const std::string &path, acmmp::Image &im) {
     im.data.resize((size_t)w * h);
     rc = acmmp_read_image_gray(path.c_str(), im.data.data(), im.data.size(), &w, &h);
     if (rc) return fail(rc, "cannot decode image %s (baseline JPEG / PGM / PFM only)", path.c_str());
+    if (!key.empty()) image_cache().put(key, im);
     return ACMMP_OK;
 }
 
