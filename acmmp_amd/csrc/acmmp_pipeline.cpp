@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -175,7 +176,7 @@ int write_png8(const std::string &path, int w, int h, int channels, const uint8_
     }
     uLongf zlen = compressBound((uLong)raw.size());
     std::vector<uint8_t> z(zlen);
-    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK)
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), Z_BEST_SPEED) != Z_OK)
         return fail(ACMMP_ERR_IO, "zlib failed for %s", path.c_str());
     z.resize(zlen);
     std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
@@ -236,8 +237,6 @@ int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
     return write_png8(path, W, H, 3, rgb.data());
 }
 
-// One view of InputInitialization (src/ACMMP.cpp:536-598): image + camera,
-// camera size from the image, rescaled to max_image_size when larger.
 // Runs fn(0..n-1) on up to 16 host threads. Returns the status of the lowest
 // failing index and leaves its message in this thread's error slot, so the
 // caller sees what the sequential loop would have reported first.
@@ -266,6 +265,8 @@ int parallel_views(int n, Fn fn) {
     return ACMMP_OK;
 }
 
+// One view of InputInitialization (src/ACMMP.cpp:536-598): image + camera,
+// camera size from the image, rescaled to max_image_size when larger.
 int load_view(const std::string &dense, int id, int max_image_size, acmmp::Image &im, acmmp_camera &cam) {
     int rc = load_image(image_path(dense, id), im);
     if (rc) return rc;
@@ -563,6 +564,27 @@ int acmmp_space_initialization(acmmp_ctx *ctx, const char *output_folder, const 
     return ACMMP_OK;
 }
 
+namespace {
+// ACMMP_HOST_TIMING=1: per-phase wall times of each ProcessProblem on stderr
+struct PhaseClock {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    std::string line;
+    PhaseClock() : on(std::getenv("ACMMP_HOST_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        char b[64];
+        std::snprintf(b, sizeof(b), " %s=%.1f", what, std::chrono::duration<double, std::milli>(now - t).count());
+        line += b;
+        t = now;
+    }
+    void print(int id) {
+        if (on) std::fprintf(stderr, "host_timing view %d ms:%s\n", id, line.c_str());
+    }
+};
+}  // namespace
+
 int acmmp_process_problem(const char *dense_folder, const char *output_folder, const acmmp_problem *problems,
                           int count, int idx, const acmmp_pass_options *opt) {
     if (!dense_folder || !output_folder || !problems || !opt || idx < 0 || idx >= count)
@@ -571,8 +593,10 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
     if (opt->verbose) std::printf("Processing image %s...\n", id8(problem.ref_image_id).c_str());
     const std::string folder = result_folder(output_folder, problem.ref_image_id);
     ::mkdir(folder.c_str(), 0777);
+    PhaseClock clk;
     try {
         acmmp::ACMMP acmmp(opt->device);
+        clk.mark("create");
         if (opt->geom_consistency) acmmp.SetGeomConsistencyParams(opt->multi_geometry != 0);
         if (opt->hierarchy) acmmp.SetHierarchyParams();
         acmmp_params p = acmmp.params();
@@ -582,7 +606,9 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
         acmmp.set_params(p);
         std::vector<acmmp::Problem> all(problems, problems + count);
         acmmp.InputInitialization(dense_folder, output_folder, all, idx);
+        clk.mark("input_init");
         acmmp.CudaSpaceInitialization(output_folder, problem);
+        clk.mark("space_init");
         const int width = acmmp.GetReferenceImageWidth(), height = acmmp.GetReferenceImageHeight();
         if (opt->seeded) {  // :275-281; GetCamera(idx) indexes this problem's cameras with the problem index
             const acmmp_params prm = acmmp.params();
@@ -593,6 +619,7 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
             acmmp.SetPlanarPrior(prior);
         }
         acmmp.RunPatchMatch();
+        clk.mark("patchmatch");
         if (opt->planar_prior) {  // :301-379
             if (opt->verbose) std::printf("Run Planar Prior Assisted PatchMatch MVS ...\n");
             if (opt->write_triangulation) {
@@ -600,10 +627,13 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
                 if (rc) return rc;
             }
             acmmp.PreparePlanarPrior();  // support points, Delaunay, prior planes; SetPlanarPriorParams
+            clk.mark("planar_prior");
             acmmp.RunPatchMatch();
+            clk.mark("patchmatch2");
         }
         const auto &planes = acmmp.GetPlaneHypotheses();
         const auto &costs = acmmp.GetCosts();
+        clk.mark("fetch");
         const size_t P = (size_t)width * height;
         std::vector<float> depths(P), normals(P * 3);
         for (size_t i = 0; i < P; ++i) {
@@ -617,9 +647,12 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
         if (!rc) rc = write_dmb(folder + "/normals.dmb", height, width, 3, normals.data());
         if (!rc) rc = write_dmb(folder + "/costs.dmb", height, width, 1, costs.data());
         if (rc) return rc;
+        clk.mark("write");
     } catch (const acmmp::Error &e) {
         return fail(e.status(), "view %d: %s", problem.ref_image_id, e.what());
     }
+    clk.mark("destroy");
+    clk.print(problem.ref_image_id);
     if (opt->verbose) std::printf("Processing image %s done!\n", id8(problem.ref_image_id).c_str());
     return ACMMP_OK;
 }
