@@ -70,8 +70,9 @@ std::string image_path(const std::string &dense, int id) {
 // Decoded-image cache. The reference re-reads and re-decodes every image of a
 // problem in every pass (src/ACMMP.cpp:536-574: each view is decoded about
 // N times per pass); here a decode is kept, keyed by path and the file's
-// inode, size and mtime (so a rewritten file is decoded again), up to
-// ACMMP_IMAGE_CACHE_MB (default 4096, 0 disables) with LRU eviction.
+// inode, size, mtime and ctime (so a rewritten file is decoded again), up to
+// ACMMP_IMAGE_CACHE_MB (default 1024: one scale of a 49-view 1600x1200 DTU
+// scan; 0 disables) with LRU eviction.
 struct ImageCache {
     struct Entry {
         std::string key;
@@ -83,7 +84,7 @@ struct ImageCache {
     size_t bytes = 0, cap = 0;
     ImageCache() {
         const char *e = std::getenv("ACMMP_IMAGE_CACHE_MB");
-        cap = (size_t)(e ? std::max(0L, std::atol(e)) : 4096L) << 20;
+        cap = (size_t)(e ? std::max(0L, std::atol(e)) : 1024L) << 20;
     }
     bool get(const std::string &key, acmmp::Image &out) {
         std::lock_guard<std::mutex> g(mu);
@@ -117,9 +118,12 @@ int load_image(const std::string &path, acmmp::Image &im) {
     struct stat st;
     std::string key;
     if (::stat(path.c_str(), &st) == 0) {
-        char b[128];
-        std::snprintf(b, sizeof(b), "|%llu|%lld|%lld.%09ld", (unsigned long long)st.st_ino, (long long)st.st_size,
-                      (long long)st.st_mtim.tv_sec, (long)st.st_mtim.tv_nsec);
+        // st_ctim too: utime() cannot set it and every write changes it, so a
+        // rewrite that keeps the size and restores the mtime is still seen
+        char b[160];
+        std::snprintf(b, sizeof(b), "|%llu|%lld|%lld.%09ld|%lld.%09ld", (unsigned long long)st.st_ino,
+                      (long long)st.st_size, (long long)st.st_mtim.tv_sec, (long)st.st_mtim.tv_nsec,
+                      (long long)st.st_ctim.tv_sec, (long)st.st_ctim.tv_nsec);
         key = path + b;
         if (image_cache().get(key, im)) return ACMMP_OK;
     }

@@ -48,12 +48,17 @@ def lpt_assign(costs: list, world: int) -> list:
 
 class DepthExchange:
     """All-gather of per-view depth maps of different sizes over a padded
-    [world * slots, Hmax, Wmax] buffer with all_gather_into_tensor."""
+    [world * slots, Hmax, Wmax] buffer with all_gather_into_tensor (RCCL has
+    no all-gatherv). The gathered maps are returned as views into one buffer
+    on `out_device` (row pitch Wmax), so a geometric pass borrows them without
+    a copy (acmmp_set_depth_maps_device takes the pitch)."""
 
-    def __init__(self, assignment: list, shapes: dict, device: torch.device, group=None):
+    def __init__(self, assignment: list, shapes: dict, device: torch.device, group=None,
+                 out_device: Optional[torch.device] = None):
         self.assignment = assignment
         self.shapes = shapes
         self.device = device
+        self.out_device = out_device or device
         self.group = group
         self.slots = max(1, max(len(a) for a in assignment))
         self.hmax = max(h for h, _ in shapes.values())
@@ -65,22 +70,28 @@ class DepthExchange:
         for k, v in enumerate(self.assignment[rank]):
             h, w = self.shapes[v]
             send[k, :h, :w] = local[v].to(self.device)
-        if world == 1:
-            recv = send
-        else:  # concatenated along dim 0: rank r's slots at [r * slots, (r + 1) * slots)
+        if dist.is_initialized():  # RCCL (nccl backend) or gloo; world size 1 included
             recv = torch.empty((world * self.slots, self.hmax, self.wmax), dtype=torch.float32, device=self.device)
             dist.all_gather_into_tensor(recv, send, group=self.group)
+        else:
+            recv = send
+        recv = recv.to(self.out_device)
+        if recv.is_cuda:
+            # the engines' HIP streams do not wait on torch's / RCCL's: the
+            # gathered maps are complete before any view borrows them
+            torch.cuda.current_stream(recv.device).synchronize()
         out = {}
-        for r in range(world):
+        for r in range(world):  # concatenated along dim 0: rank r's slots at [r * slots, (r + 1) * slots)
             for k, v in enumerate(self.assignment[r]):
                 h, w = self.shapes[v]
-                out[v] = recv[r * self.slots + k, :h, :w].contiguous()
+                out[v] = recv[r * self.slots + k, :h, :w]
         return out
 
 
 @dataclass
 class ViewTask:
-    """Everything one ProcessProblem call needs, in memory."""
+    """Everything one ProcessProblem call needs, resident on the tensor
+    device."""
     index: int                 # problem index
     ref_id: int
     ids: list                  # image ids, ref first
@@ -93,44 +104,61 @@ class ViewTask:
     seed_lo: int
     seed_hi: int
     max_iterations: int
-    depths: Optional[list] = None          # source depth maps (tensors) for geom passes
-    state: Optional[tuple] = None          # (planes (H,W,4), costs (H,W)) numpy, geom passes
+    depths: Optional[list] = None          # source depth maps (tensor views, any row pitch), geom passes
+    state: Optional[tuple] = None          # (planes (H,W,4), costs (H,W)) tensors, geom passes
     hier_inputs: Optional[tuple] = None    # (scaled planes (sh,sw,4), upsampled depth (H,W)) numpy
 
 
 @dataclass
 class ViewResult:
-    planes: np.ndarray   # (H, W, 4): world normal xyz + depth
-    costs: np.ndarray    # (H, W)
+    planes: torch.Tensor   # (H, W, 4): world normal xyz + depth
+    costs: torch.Tensor    # (H, W)
     extra: dict = field(default_factory=dict)
 
 
-def engine_compute(device: int) -> Callable[[ViewTask], ViewResult]:
+def _view_params(t: ViewTask) -> _abi.Params:
+    """ProcessProblem's parameter set-up (src/acmmp_definitions.cpp:253-268):
+    defaults, SetGeomConsistencyParams (geom: 2 iterations, src/ACMMP.cpp:
+    447-454), SetHierarchyParams, the per-view RNG key, -iterations."""
+    p = _abi.default_params()
+    if t.geom:
+        p.geom_consistency = 1
+        p.max_iterations = 2
+        if t.multi:
+            p.multi_geometry = 1
+    if t.hierarchy:
+        p.hierarchy = 1
+    p.seed_lo = t.seed_lo & 0xFFFFFFFF
+    p.seed_hi = t.seed_hi & 0xFFFFFFFF
+    if t.max_iterations > 0:
+        p.max_iterations = t.max_iterations
+    return p
+
+
+def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
     """ProcessProblem's per-view work (src/acmmp_definitions.cpp:260-379) on
-    the GPU engine, with images / depth maps borrowed from HBM."""
-
-    def run(t: ViewTask) -> ViewResult:
-        with ACMMP(device) as eng:
-            if t.geom:
-                eng.SetGeomConsistencyParams(t.multi)
-            if t.hierarchy:
-                eng.SetHierarchyParams()
-            eng.update_params(seed_lo=t.seed_lo & 0xFFFFFFFF, seed_hi=t.seed_hi & 0xFFFFFFFF)
-            if t.max_iterations > 0:
-                eng.update_params(max_iterations=t.max_iterations)
-            eng.set_images_device(t.cams, [im.data_ptr() for im in t.images])
-            if t.geom:
-                eng.set_depth_maps_device([d.data_ptr() for d in t.depths])
-                eng.set_plane_hypotheses(*t.state)
-            if t.hierarchy:
-                eng.set_hierarchy_inputs(*t.hier_inputs)
-            eng.RunPatchMatch()
-            if t.planar:
-                eng.prepare_planar_prior()
-                eng.RunPatchMatch()
-            return ViewResult(eng.plane_hypotheses(), eng.costs())
-
-    return run
+    a pooled engine: images, previous state and source depth maps borrowed
+    from HBM, results exported device-to-device into fresh tensors (the
+    previous pass's tensors may still be read by the .dmb writers)."""
+    ref = t.images[0]
+    H, W = ref.shape
+    planes = torch.empty((H, W, 4), dtype=torch.float32, device=ref.device)
+    costs = torch.empty((H, W), dtype=torch.float32, device=ref.device)
+    eng.set_params(_view_params(t))
+    eng.set_images_device(t.cams, [im.data_ptr() for im in t.images], [im.stride(0) for im in t.images])
+    if t.geom:
+        eng.set_depth_maps_device([d.data_ptr() for d in t.depths], [d.stride(0) for d in t.depths])
+        eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
+    if t.hierarchy:
+        eng.set_hierarchy_inputs(*t.hier_inputs)
+    eng.run_async()
+    if t.planar:
+        eng.synchronize()
+        eng.prepare_planar_prior()
+        eng.run_async()
+    eng.export_results(planes.data_ptr(), costs.data_ptr(), 0)
+    eng.synchronize()
+    return ViewResult(planes, costs)
 
 
 def gpu_jbu(device: int):
@@ -141,13 +169,20 @@ def gpu_jbu(device: int):
 
 class ViewParallelPipeline:
     """main_ACMMP's multi-scale pass loop (src/main_ACMMP.cpp:96-176), views
-    sharded over the ranks of `group` (default: the world)."""
+    sharded over the ranks of `group` (default: the world).
+
+    Device-resident (multi-GPU keeps maps resident and writes
+    .dmb at pass end): images stay in HBM per scale, every view's planes /
+    costs stay on the device between passes, the gathered depth maps are
+    borrowed in place, one pool of engines (one HIP stream each) is reused
+    for every view and pass, and the .dmb files are written by a writer pool
+    from device-to-host copies while the next pass computes."""
 
     def __init__(self, dense_folder: str, output_dir: str = "/ACMMP", device: int = 0, seed: int = 1234,
                  max_iterations: int = 0, geom_iterations: int = 2, group=None,
                  compute: Optional[Callable] = None, jbu: Optional[Callable] = None, write_outputs: bool = True,
                  comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None,
-                 concurrent_views: int = 1):
+                 concurrent_views: int = 2):
         self.dense = dense_folder
         self.output_folder = dense_folder + output_dir
         self.device = device
@@ -157,13 +192,14 @@ class ViewParallelPipeline:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.compute = compute or engine_compute(device)
+        self.compute = compute or engine_compute
         self.jbu = jbu or gpu_jbu(device)
         self.write_outputs = write_outputs
-        # views of a pass computed at once (each on its own engine / HIP stream,
-        # from a thread: ctypes drops the GIL in every library call), so one
-        # view's launches fill the tail of another's and host copies overlap
+        # views of a pass computed at once (each on its own pooled engine /
+        # HIP stream, from a thread: ctypes drops the GIL in every library
+        # call), so one view's launches fill the tail of another's
         self.concurrent_views = max(int(concurrent_views), 1)
+        self.pool = None
         self._writer = None  # .dmb writer pool (created on the first write)
         self._pending = []
         if tensor_device is None:
@@ -182,8 +218,8 @@ class ViewParallelPipeline:
             costs.append(float(w * h * max(p.num_src_images, 1)))
         self.assignment = lpt_assign(costs, self.world)
         self.mine = self.assignment[self.rank]
-        self.state = {}     # own views: ref_id -> ViewResult (latest pass)
-        self.depths = {}    # every view: ref_id -> depth tensor (previous pass, gathered)
+        self.state = {}     # own views: problem index -> ViewResult (latest pass)
+        self.depths = {}    # every view: problem index -> depth tensor view (previous pass, gathered)
         self.pass_index = 0
 
     # ------------------------------------------------------------- inputs
@@ -229,6 +265,13 @@ class ViewParallelPipeline:
         for i, (img, cam) in zip(order, loaded):
             self.images[i] = torch.from_numpy(img).to(self.tdev)
             self.cams[i] = cam
+        self._sync()
+
+    def _sync(self):
+        """Torch's queued work on the tensor device is complete (the engines'
+        streams do not wait on torch's stream)."""
+        if self.tdev.type == "cuda":
+            torch.cuda.current_stream(self.tdev).synchronize()
 
     def _shapes(self):
         shapes = {}
@@ -242,8 +285,15 @@ class ViewParallelPipeline:
         return shapes
 
     # --------------------------------------------------------------- pass
+    def _map(self, tasks):
+        if self.compute is not engine_compute:  # injected stand-in (CPU tests): no engines
+            return [self.compute(t, None) for t in tasks]
+        if self.pool is None:
+            from .resident import EnginePool
+            self.pool = EnginePool(self.device, self.concurrent_views)
+        return self.pool.map(lambda eng, t: self.compute(t, eng), tasks)
+
     def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
-        local = {}
         tasks = []
         for v in self.mine:
             p = self.problems[v]
@@ -253,7 +303,7 @@ class ViewParallelPipeline:
                          multi=multi, seed_lo=self.seed + p.ref_image_id, seed_hi=self.pass_index,
                          max_iterations=self.max_iterations)
             if geom:
-                t.depths = [self.depths[self.index_of[i]].to(self.tdev) for i in ids]
+                t.depths = [self.depths[self.index_of[i]] for i in ids]
                 prev = self.state[v]
                 t.state = (prev.planes, prev.costs)
             if hierarchy:
@@ -262,21 +312,18 @@ class ViewParallelPipeline:
                 up = prev.extra["jbu_depth"]
                 sh, sw = prev.costs.shape
                 upsample = sw != H or sh != W  # src/ACMMP.cpp:766, rows/cols swap included
-                w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
-                scaled = np.concatenate([prev.planes[..., :3], w[..., None]], -1).astype(np.float32)
+                pc = prev.costs.cpu().numpy()
+                w = pc if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
+                scaled = np.concatenate([prev.planes[..., :3].cpu().numpy(), w[..., None]], -1).astype(np.float32)
                 t.hier_inputs = (scaled, up)
             tasks.append(t)
-        if self.concurrent_views > 1 and len(tasks) > 1:
-            from concurrent.futures import ThreadPoolExecutor
-            with ThreadPoolExecutor(max_workers=self.concurrent_views) as ex:
-                results = list(ex.map(self.compute, tasks))
-        else:
-            results = [self.compute(t) for t in tasks]
-        self._flush_writes()  # the previous pass's files are complete before this pass rewrites them
+        self._sync()
+        results = self._map(tasks)
+        local = {}
         for t, res in zip(tasks, results):  # in view order, as the sequential loop
             v = t.index
             self.state[v] = res
-            local[v] = torch.from_numpy(np.ascontiguousarray(res.planes[..., 3]))
+            local[v] = res.planes[..., 3]
             if self.write_outputs:
                 self._write(t.ref_id, res, geom)
         self.depths = exchange.gather(self.rank, local)
@@ -284,54 +331,80 @@ class ViewParallelPipeline:
 
     def _write(self, ref_id: int, res: ViewResult, geom: bool):
         """Queues the view's three .dmb files on the writer pool: they are
-        outputs only (nothing in this driver reads them back), so they are
-        written while the next pass computes. A pass's writes start after the
-        previous pass's finished (the same files are rewritten every pass)."""
+        outputs only (nothing in this driver reads them back), so the device-
+        to-host copies and the writes run while the next pass computes. Each
+        pass's results are fresh tensors, so no later pass overwrites what a
+        writer still reads; the files of one view are written in pass order
+        (a view's writes go to one writer thread)."""
         folder = aio.result_folder(self.output_folder, ref_id)
         os.makedirs(folder, exist_ok=True)
+        planes, costs = res.planes, res.costs
 
         def write():
-            aio.write_dmb(os.path.join(folder, "depths_geom.dmb" if geom else "depths.dmb"), res.planes[..., 3])
-            aio.write_dmb(os.path.join(folder, "normals.dmb"), res.planes[..., :3])
-            aio.write_dmb(os.path.join(folder, "costs.dmb"), res.costs)
+            pl = planes.cpu().numpy()
+            aio.write_dmb(os.path.join(folder, "depths_geom.dmb" if geom else "depths.dmb"), pl[..., 3])
+            aio.write_dmb(os.path.join(folder, "normals.dmb"), pl[..., :3])
+            aio.write_dmb(os.path.join(folder, "costs.dmb"), costs.cpu().numpy())
 
         if self._writer is None:
             from concurrent.futures import ThreadPoolExecutor
-            self._writer = ThreadPoolExecutor(max_workers=4)
-        self._pending.append(self._writer.submit(write))
+            self._writer = [ThreadPoolExecutor(max_workers=1) for _ in range(4)]
+        self._pending.append(self._writer[ref_id % len(self._writer)].submit(write))
 
     def _flush_writes(self):
         pending, self._pending = self._pending, []
+        first = None
         for f in pending:
-            f.result()  # re-raises a write error
+            try:
+                f.result()
+            except BaseException as e:  # every write is awaited; the first error is raised
+                first = first or e
+        if first is not None:
+            raise first
+
+    def _shutdown(self):
+        if self._writer is not None:
+            for w in self._writer:
+                w.shutdown()
+            self._writer = None
+        if self.pool is not None:
+            self.pool.close()
+            self.pool = None
 
     def run(self) -> str:
         os.makedirs(self.output_folder, exist_ok=True)
         max_down = self.max_num_downscale
         first = True
-        while max_down >= 0:
-            pipeline.scale_step(self.problems)
-            self._load_views()
-            exchange = DepthExchange(self.assignment, self._shapes(), self.cdev, self.group)
-            if first:
-                first = False
-                self.run_pass(False, True, False, False, exchange)
-            else:
-                for v in self.mine:  # JointBilateralUpsampling, in memory
-                    p = self.problems[v]
-                    img = self.images[p.ref_image_id].cpu().numpy()
-                    up, isc = self.jbu(img, self.state[v].planes[..., 3])
-                    if up is None:
-                        raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
-                    self.state[v].extra["jbu_depth"] = up
-                self.run_pass(False, True, True, False, exchange)
-            for g in range(self.geom_iterations):
-                self.run_pass(True, False, False, g > 0, exchange)
-            max_down -= 1
-        self._flush_writes()
-        if self._writer is not None:
-            self._writer.shutdown()
-            self._writer = None
+        try:
+            while max_down >= 0:
+                pipeline.scale_step(self.problems)
+                self._load_views()
+                exchange = DepthExchange(self.assignment, self._shapes(), self.cdev, self.group,
+                                         out_device=self.tdev)
+                if first:
+                    first = False
+                    self.run_pass(False, True, False, False, exchange)
+                else:
+                    for v in self.mine:  # JointBilateralUpsampling, in memory
+                        p = self.problems[v]
+                        img = self.images[p.ref_image_id].cpu().numpy()
+                        up, isc = self.jbu(img, self.state[v].planes[..., 3].cpu().numpy())
+                        if up is None:
+                            raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
+                        self.state[v].extra["jbu_depth"] = up
+                    self.run_pass(False, True, True, False, exchange)
+                for g in range(self.geom_iterations):
+                    self.run_pass(True, False, False, g > 0, exchange)
+                max_down -= 1
+            self._flush_writes()
+        except BaseException:
+            try:
+                self._flush_writes()  # no write is left running; the pass's error wins
+            except BaseException:
+                pass
+            raise
+        finally:
+            self._shutdown()
         if dist.is_initialized() and self.world > 1:
             dist.barrier(group=self.group)
         return self.output_folder

@@ -7,25 +7,28 @@ Workload (BASELINE.json configs[1], "cfg2"): per GPU, 10 reference views at
 all-gather of the depth maps, then a geometric-consistency pass over the same
 views (it reads the neighbours' depth maps: the real exchange step).
 
-One "step" = photometric pass + all-gather + geometric pass. Weak scaling:
-every rank owns one copy of the 10-view cfg2 problem (global view ids
-rank*10 + k), so per-GPU work is identical for every N; the depth maps of all
-ranks are all-gathered (RCCL over xGMI) and the geometric pass reads its
-sources from the gathered buffer. Inputs are rendered straight into HBM before
-timing (synthetic, seeded).
+One "step" = photometric pass + all-gather + geometric pass, run by
+`acmmp_amd.resident` (the same code the parity test
+tests/test_gpu_headline.py drives): images, plane/cost state and depth maps
+stay in HBM, every RunPatchMatch's results are exported device-to-device.
+Weak scaling: every rank owns one copy of the 10-view cfg2 problem (global
+view ids rank*10 + k), so per-GPU work is identical for every N.
 
-value = total pixels processed by all ranks (2 passes x views x W x H) /
-max-over-ranks wall time of the K timed steps, in Mpix/s. Each GPU keeps two
-views in flight (two engines, each on its own HIP stream, --streams 2): the
-tail of one view's sweep launch fills with the other's blocks.
+value = RunPatchMatch pixels processed by all ranks (2 passes x views x W x H)
+/ max-over-ranks wall time of the K timed steps, in Mpix/s (per pass; a
+reference view's photometric + geometric result is value / 2).
+
+Rank 0 at N=1 also runs, BEFORE touching the GPU, two rocprofv3 counter
+passes of one step (tools/bench_pmc.py) for the roofline block, and after the
+timed region the CPU oracle on a bounded sample (cpu_baseline).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -37,17 +40,17 @@ BASELINE_METRIC = "Mpixels/sec PatchMatch (1600×1200, 8 iters) at 1/2/4/8 GPUs;
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes_per_pixel_iter(num_images: int, geom: bool) -> int:
+def logical_bytes_per_pixel_iter(num_images: int, geom: bool) -> int:
     """SURVEY §8d / BASELINE.md §3 gather-byte model per pixel-iteration:
     14*(N-1) NCC calls x 724 B + 572 B of state, + 14*(N-1)*4 B in geometric
-    passes."""
+    passes. Logical bytes (counted as if nothing were cached)."""
     b = 14 * (num_images - 1) * 724 + 572
     if geom:
         b += 14 * (num_images - 1) * 4
     return b
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -59,21 +62,49 @@ def parse():
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="800x600", help="ref-view crop timed on the CPU oracle")
-    ap.add_argument("--profile-dir", default=None, help="write per-run timing JSON here")
     ap.add_argument("--streams", type=int, default=2,
                     help="engines (HIP streams) per GPU running different views concurrently")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to test on one GPU)")
-    return ap.parse_args()
+                    help="collective backend (nccl = RCCL over xGMI; gloo only to test on one GPU)")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                    help="in-run rocprofv3 counter passes for the roofline (rank 0, N=1)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def host_cpu():
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
 
 
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    pmc = None
+    if args.pmc == "auto" and not args.pmc_child and "WORLD_SIZE" not in os.environ:
+        # counter passes first: child processes, before this process touches the GPU
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_pmc
+        child = ["--views", str(args.views), "--nsrc", str(args.nsrc), "--width", str(args.width),
+                 "--height", str(args.height), "--iters", str(args.iters), "--steps", "1", "--warmup", "0"]
+        pmc = bench_pmc.collect(os.path.abspath(__file__), child, os.path.join(ROOT, "gpurun_out", "bench_pmc"))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    world, rank = world_env, rank_env
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -81,22 +112,22 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     backend = args.backend
-    if world > 1:
+    # launched by torch.distributed.run (WORLD_SIZE in the env): a process
+    # group even at world size 1, so the RCCL all-gather runs in every case
+    distributed = "WORLD_SIZE" in os.environ and not args.pmc_child
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
 
-    from acmmp_amd import ACMMP, default_params, scene
+    from acmmp_amd import default_params, scene
+    from acmmp_amd.resident import EnginePool, ResidentViews, geometric_view, photometric_view
 
-    # Weak scaling: every rank owns one copy of the cfg2 problem (the same
-    # 10-view arc, so per-GPU work is identical for every N); global view id
-    # = rank * views + k. The depth maps of ALL ranks are all-gathered between
-    # the passes and the geometric pass reads its sources from the gathered
-    # buffer, as a view-parallel pipeline does.
     if args.views < args.nsrc + 1:
         raise SystemExit(f"--views {args.views} cannot supply {args.nsrc} source views per problem")
+    streams = 1 if args.pmc_child else args.streams
     V = args.views * world
     W, H = args.width, args.height
     setup = scene.scene_setup(num_views=args.views, width=W, height=H)
@@ -108,138 +139,70 @@ def main():
     torch.cuda.synchronize()
 
     n_img = 1 + args.nsrc
-    planes = torch.empty((args.views, H, W, 4), dtype=torch.float32, device=device)
-    costs = torch.empty((args.views, H, W), dtype=torch.float32, device=device)
-    my_depth = torch.empty((args.views, H, W), dtype=torch.float32, device=device)
-    all_depth = torch.empty((V, H, W), dtype=torch.float32, device=device) if world > 1 else my_depth
-
-    # one engine (own HIP stream) per concurrent view: with --streams > 1 the
-    # views of a pass run in rounds of `streams`, their kernels overlapping on
-    # the GPU (the tail of one view's launch fills with the other's blocks)
-    engines = [ACMMP(dev_index) for _ in range(max(args.streams, 1))]
-    for e in engines:
-        e.set_timing(True)
-    base = default_params()
-    base.max_iterations = args.iters
-
-    sweep_stats = {"photo": [0.0, 0], "geom": [0.0, 0]}
-
-    def launch_view(eng, k: int, v: int, geom: bool):
-        ids = [v] + srcs[v]
-        eng.set_params(base)
-        eng.set_images_device([cams[i] for i in ids], [images[i].data_ptr() for i in ids])
-        if geom:
-            p = eng.params
-            p.geom_consistency = 1
-            p.max_iterations = args.iters  # BASELINE cfg2: 8 iterations in both passes
-            eng.set_params(p)
-            # global view ids index the gathered maps (world == 1: my_depth)
-            eng.set_depth_maps_device([all_depth[i].data_ptr() for i in ids])
-            eng.set_plane_hypotheses_device(planes[k].data_ptr(), costs[k].data_ptr())
-        eng.run_async()
-        if not geom:
-            eng.export_results(planes[k].data_ptr(), costs[k].data_ptr(), my_depth[k].data_ptr())
-
-    stats_lock = threading.Lock()
-
-    def finish_view(eng, geom: bool):
-        eng.synchronize()
-        t = eng.timing()
-        with stats_lock:
-            st = sweep_stats["geom" if geom else "photo"]
-            st[0] += t["sweep_ms"]
-            st[1] += t["sweep_launches"]
-
-    def run_pass(geom: bool):
-        # one host thread per engine takes the next view off a shared queue as
-        # soon as its own previous view finished (no lockstep rounds, so a view
-        # that ends early does not leave the GPU to its partner's tail); the
-        # library calls release the GIL (ctypes)
-        work = list(enumerate(mine))
-        if len(engines) == 1:
-            for k, v in work:
-                launch_view(engines[0], k, v, geom)
-                finish_view(engines[0], geom)
-            return
-        errors = []
-
-        def worker(eng):
-            try:
-                while True:
-                    with stats_lock:
-                        if not work or errors:
-                            return
-                        k, v = work.pop(0)
-                    launch_view(eng, k, v, geom)
-                    finish_view(eng, geom)
-            except BaseException as e:  # re-raised on the main thread
-                with stats_lock:
-                    errors.append(e)
-
-        threads = [threading.Thread(target=worker, args=(e,)) for e in engines]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
-
+    pool = EnginePool(dev_index, streams, timing=True)
+    rv = ResidentViews(pool, cams, images, srcs, mine, H, W, total_views=V if distributed else None)
+    all_depth = rv.all_depth
+    photo_params = default_params()
+    photo_params.max_iterations = args.iters
+    geom_params = default_params()
+    geom_params.max_iterations = args.iters  # BASELINE cfg2: 8 iterations in both passes
+    geom_params.geom_consistency = 1
+    work = list(enumerate(mine))
 
     def step():
-        run_pass(geom=False)
-        if world > 1:
+        rv.photometric_pass(photo_params)
+        if distributed:
             if backend == "nccl":  # RCCL over xGMI, device buffers
-                dist.all_gather_into_tensor(all_depth, my_depth)
+                dist.all_gather_into_tensor(rv.all_depth, rv.my_depth)
             else:  # gloo (tests on one GPU): staged through host memory
                 host = torch.empty((V, H, W), dtype=torch.float32)
-                dist.all_gather_into_tensor(host, my_depth.cpu())
-                all_depth.copy_(host)
+                dist.all_gather_into_tensor(host, rv.my_depth.cpu())
+                rv.all_depth.copy_(host)
+            # the engines' streams do not wait on torch's/RCCL's: finish the
+            # gather before a geometric view borrows all_depth
             torch.cuda.synchronize()
-        run_pass(geom=True)
+        rv.geometric_pass(geom_params)
 
     for _ in range(args.warmup):
         step()
-    for st in sweep_stats.values():
-        st[0], st[1] = 0.0, 0
-    if world > 1:
+    pool.reset_timing()
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed and world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    timed_ms, timed_launches = pool.sweep_ms, pool.sweep_launches
+    if args.pmc_child:
+        pool.close()
+        return
+
+    # one photometric + one geometric view alone on one stream: the
+    # un-overlapped duration of a k_sweep launch (HIP events on the engine's
+    # stream), the denominator of the roofline fractions
+    iso_pool = EnginePool(dev_index, 1, timing=True)
+    eng = iso_pool.engines[0]
+    k0, v0 = work[0]
+    ids0 = [v0] + srcs[v0]
+    photometric_view(iso_pool, eng, photo_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
+                     rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr(), rv.my_depth[k0].data_ptr())
+    geometric_view(iso_pool, eng, geom_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
+                   [all_depth[i].data_ptr() for i in ids0], rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr())
+    iso_ms = iso_pool.sweep_ms / max(iso_pool.sweep_launches, 1)
+    iso_pool.close()
 
     pix_total = 2 * args.views * world * W * H * args.steps
     value = pix_total / elapsed / 1e6
-    # roofline of the dominant kernel (k_sweep), timed with hipEvents on the
-    # engine stream: algorithmic bytes per launch / mean launch time
     P = W * H
-    bytes_photo = (P / 2) * algorithmic_bytes_per_pixel_iter(n_img, False) * sweep_stats["photo"][1]
-    bytes_geom = (P / 2) * algorithmic_bytes_per_pixel_iter(n_img, True) * sweep_stats["geom"][1]
-    sweep_ms = sweep_stats["photo"][0] + sweep_stats["geom"][0]
-    launches = sweep_stats["photo"][1] + sweep_stats["geom"][1]
-    # with S engines running S views at a time, S sweep launches overlap on the
-    # GPU: each one's HIP-event duration (what rocprofv3 also reports) spans
-    # the shared time, so the kernel's own rate uses duration / S
-    S = len(engines)
-    achieved = (bytes_photo + bytes_geom) / (sweep_ms / S / 1e3) / 1e9 if sweep_ms > 0 else 0.0
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_sweep.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("width") == W and pmc.get("height") == H and pmc.get("num_images") == n_img:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    logical = (P / 2) * (logical_bytes_per_pixel_iter(n_img, False) + logical_bytes_per_pixel_iter(n_img, True)) / 2
     result = {
         "metric": BASELINE_METRIC,
         "value": round(value, 4),
@@ -261,52 +224,119 @@ def main():
             "height": H,
             "num_images": n_img,
             "iters": args.iters,
-            "parallelism": f"view-parallel x{world} (one process per GPU, {'RCCL' if backend == 'nccl' else 'gloo'} "
-                           f"all-gather of depth maps between the passes; {S} views in flight per GPU on "
-                           f"{S} HIP streams)",
+            "parallelism": f"view-parallel x{world} (one process per GPU, "
+                           f"{('RCCL' if backend == 'nccl' else 'gloo') if distributed else 'no'} "
+                           f"all-gather of depth maps between the passes; {streams} views in flight per GPU on "
+                           f"{streams} HIP streams)",
+            "value_counts": "RunPatchMatch pixels (2 passes per view); per reference view (photometric + "
+                            f"geometric) = {value / 2:.2f} Mpix/s",
+            "residency": "images, state and depth maps stay in HBM; results exported device-to-device "
+                         "(no per-run D2H copy as in the reference's RunPatchMatch, src/ACMMP.cu:1453-1454)",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "k_sweep (CheckerboardPropagation)",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "model": "gather-byte model, SURVEY §8d: B_iter = 14*(N-1)*724 + 572 (+14*(N-1)*4 geom) "
-                     "bytes per pixel-iteration, P/2 pixels per launch",
-            "note": "gather bytes are logical (counted as if uncached, BASELINE.md §3); frac > 1 means "
-                    "they are served from LDS/L1/L2 — traffic is the PMC-measured memory-side fetch+write",
-            "sweep_launches": launches,
-            "mean_launch_ms": round(sweep_ms / max(launches, 1), 3),
-            "concurrent_launches": S,
-            "effective_launch_ms": round(sweep_ms / S / max(launches, 1), 3),
-            "timing": "achieved = algorithmic bytes per launch / effective_launch_ms; mean_launch_ms is the "
-                      "HIP-event duration of one launch while S views' launches share the GPU (S engine "
-                      "streams), the figure rocprofv3's kernel stats report for the same command",
-        },
+        "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, streams),
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, setup, images, cams, srcs, mine)
+        result["cpu_baseline"] = cpu_baseline(args, setup, images, cams, srcs, mine, all_depth, value)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    for e in engines:
-        e.close()
-    if world > 1:
+    pool.close()
+    if distributed:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, setup, images, cams, srcs, mine):
-    """CPU oracle (oracle/acmmp_oracle.c, OpenMP) timed on a bounded sample of
-    the same workload: a crop of the first reference view (principal point
-    shifted) against its full-size source views, photometric, same iterations.
-    Per-pixel work equals the full run's."""
+def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
+    """The dominant kernel's roofline (k_sweep, >90 % of the step's GPU time).
+
+    k_sweep is bound by the texture-data (TD) path that serves its
+    buffer_load gathers, so the binding roofline is that
+    unit's: achieved = gather wave-instructions per second, peak = the rate
+    at which the TD would be 100 % busy at the measured TD cycles per
+    instruction (256 CUs x clock / cycles per instruction), frac = TD busy
+    fraction. The HBM roofline is reported beside it from the memory-side
+    counter bytes. Durations: the un-overlapped HIP-event time of one launch
+    (iso_ms, one stream); rocprofv3's profiled duration is in `pmc`."""
+    out = {
+        "bound": "td-gather",
+        "kernel": "k_sweep (CheckerboardPropagation)",
+        "launch_ms": round(iso_ms, 3),
+        "launch_ms_note": "HIP events on the engine stream, one launch alone (one photometric + one geometric "
+                          "view on one stream after the timed region); in the timed region "
+                          f"{streams} views share the GPU and a launch spans "
+                          f"{timed_ms / max(timed_launches, 1):.3f} ms",
+        "logical_gather_GBs": round(logical_bytes / (iso_ms / 1e3) / 1e9, 1),
+        "logical_note": "SURVEY §8d / BASELINE.md §3 model (36 samples x 5 texels x 4 B per NCC, counted as if "
+                        "uncached) per launch / launch_ms: a data-volume figure, not an HBM fraction",
+    }
+    if not pmc or "error" in pmc:
+        out.update({"achieved": None, "peak": None, "unit": "Ginst/s", "frac": None, "traffic": None,
+                    "pmc": (pmc or {}).get("error", "counter passes skipped")})
+        return out
+    clock_hz = pmc["clock_ghz"] * 1e9
+    insts = pmc["gather_insts"]
+    achieved = insts / (iso_ms / 1e3) / 1e9
+    peak = 256 * clock_hz / pmc["td_cyc_per_inst"] / 1e9
+    hbm_gbs = pmc["hbm_bytes"] / (iso_ms / 1e3) / 1e9
+    out.update({
+        "achieved": round(achieved, 2),
+        "peak": round(peak, 2),
+        "unit": "Ginst/s",
+        "frac": round(pmc["td_busy_frac"], 4),
+        "traffic": round(pmc["hbm_bytes"]),
+        "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per launch / launch_ms; peak = 256 CUs x clock "
+                 "(GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / TA_BUFFER_READ_WAVEFRONTS_sum); "
+                 "frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8)",
+        "hbm": {
+            "bound": "hbm",
+            "achieved": round(hbm_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
+            "traffic": round(pmc["hbm_bytes"]),
+            "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 "
+                    "(Infinity-Cache hits included), FETCH doubled per the gfx950 calibration",
+        },
+        "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
+    })
+    return out
+
+
+def cpu_baseline(args, setup, images, cams, srcs, mine, all_depth, gpu_value):
+    """CPU oracle (oracle/acmmp_oracle.c, OpenMP) on bounded samples of the
+    same work: (1) cfg1 in full (5 views 400x300, 3 iters, photometric);
+    (2) the cfg2 step on a crop of reference view 0 (principal point shifted)
+    against its full-size source views: photometric, then geometric with the
+    GPU's photometric depth maps of the sources, 8 iterations each — the
+    per-pixel work of the GPU step."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: baseline leg only
-    from acmmp_amd import default_params
+    from acmmp_amd import ACMMP, default_params, scene
     from acmmp_amd._abi import Camera
 
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    model, ncpu, avail = host_cpu()
+    oracle.build()
+
+    # (1) cfg1 in full, CPU and GPU, same N and iterations
+    sc1 = scene.make_scene(num_views=5, width=400, height=300)
+    c1, i1 = sc1.problem(0, 4)
+    p1 = default_params()
+    p1.max_iterations = 3
+    with ACMMP(0) as eng:
+        eng.set_params(p1)
+        eng.set_images(c1, i1)
+        prm1 = eng.params
+        eng.RunPatchMatch()  # warm
+        g0 = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            eng.RunPatchMatch()
+        g1 = (time.perf_counter() - g0) / reps
+    t0 = time.perf_counter()
+    oracle.run_patchmatch(prm1, c1, i1, nthreads=threads)
+    t1 = time.perf_counter() - t0
+
+    # (2) cfg2 crop, photometric + geometric
     cw, ch = (int(v) for v in args.cpu_sample.split("x"))
     v = mine[0]
     ids = [v] + srcs[v]
@@ -324,18 +354,39 @@ def cpu_baseline(args, setup, images, cams, srcs, mine):
     p.max_iterations = args.iters
     p.depth_min = cs[0].depth_min * 0.6
     p.depth_max = cs[0].depth_max * 1.2
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    oracle.build()
+    depths = [all_depth[i].cpu().numpy() for i in ids]
     t0 = time.perf_counter()
-    oracle.run_patchmatch(p, cs, imgs, nthreads=threads)
-    dt = time.perf_counter() - t0
+    ph = oracle.run_patchmatch(p, cs, imgs, nthreads=threads)
+    t_photo = time.perf_counter() - t0
+    depths[0] = np.ascontiguousarray(ph["planes"][..., 3])
+    pg = default_params()
+    pg.max_iterations = args.iters
+    pg.geom_consistency = 1
+    pg.depth_min, pg.depth_max = p.depth_min, p.depth_max
+    t0 = time.perf_counter()
+    oracle.run_patchmatch(pg, cs, imgs, depths=depths, planes=ph["planes"], costs=ph["costs"], nthreads=threads)
+    t_geom = time.perf_counter() - t0
+    cpu_value = 2 * cw * ch / (t_photo + t_geom) / 1e6
     return {
-        "value": round(cw * ch / dt / 1e6, 5),
+        "value": round(cpu_value, 5),
         "unit": "Mpix/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{cw}x{ch} crop of ref view {v} (K shifted) vs {len(ids) - 1} full {args.width}x{args.height} "
-                  f"source views, {args.iters} iters, photometric, {dt:.2f} s",
+                  f"source views, {args.iters} iters, photometric {t_photo:.2f} s + geometric {t_geom:.2f} s "
+                  f"(the GPU step's per-pixel work)",
+        "cpu_model": model,
+        "nproc": ncpu,
+        "cpus_available": avail,
+        "speedup_gpu_vs_cpu": round(gpu_value / cpu_value, 1),
+        "cfg1": {
+            "workload": "5 views 400x300, 3 iters, photometric (BASELINE configs[0]), in full",
+            "cpu_s": round(t1, 3),
+            "gpu_s": round(g1, 5),
+            "cpu_mpix_s": round(400 * 300 / t1 / 1e6, 4),
+            "gpu_mpix_s": round(400 * 300 / g1 / 1e6, 2),
+            "speedup": round(t1 / g1, 1),
+        },
     }
 
 

@@ -33,15 +33,16 @@ def test_lpt_assign():
     assert lpt_assign([1, 2], 4)[2:] == [[], []]
 
 
-def fake_compute(t):
+def fake_compute(t, eng=None):
     """Deterministic stand-in for ProcessProblem's engine work: depends on the
-    view's images, on every source depth map (geom) and on its own state."""
+    view's images, on every source depth map (geom) and on its own state.
+    Tensors in, tensors out, like the real engine_compute."""
     img = t.images[0].cpu().numpy().astype(np.float64)
     H, W = img.shape
     depth = 500.0 + img / 10.0 + 3.0 * t.seed_hi
     if t.geom:
         depth = depth + sum(float(d.cpu().double().mean()) for d in t.depths) / 100.0
-        depth = depth + t.state[0][..., 3] / 1000.0 + (7.0 if t.multi else 0.0)
+        depth = depth + t.state[0][..., 3].cpu().numpy() / 1000.0 + (7.0 if t.multi else 0.0)
     if t.hierarchy:
         depth = depth + t.hier_inputs[1] / 100.0 + float(t.hier_inputs[0].mean())
     planes = np.zeros((H, W, 4), np.float32)
@@ -50,7 +51,7 @@ def fake_compute(t):
     costs = (img / 255.0).astype(np.float32)
     if t.planar:
         costs = costs * 0.5
-    return ViewResult(planes, costs)
+    return ViewResult(torch.from_numpy(planes), torch.from_numpy(costs))
 
 
 def fake_jbu(image, depth):

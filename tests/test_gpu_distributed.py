@@ -26,11 +26,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, dense, q):
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+def _worker(rank, world, port, dense, q, backend="gloo", out="/VP2"):
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+        comm = torch.device("cuda", 0)  # RCCL: the all-gather runs on device buffers
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        comm = torch.device("cpu")
     try:
-        pipe = ViewParallelPipeline(dense, "/VP2", device=0, tensor_device=torch.device("cuda", 0),
-                                    comm_device=torch.device("cpu"))
+        pipe = ViewParallelPipeline(dense, out, device=0, tensor_device=torch.device("cuda", 0),
+                                    comm_device=comm)
         pipe.run()
         q.put((rank, pipe.mine))
     finally:
@@ -58,16 +65,64 @@ def test_world1_matches_oracle_jacobi(dense, jacobi_maps, concurrent):
     assert _compare(out, jacobi_maps) == 5 * 4
 
 
-def test_world2_matches_oracle_jacobi(dense, jacobi_maps):
+def _spawn(world, dense, backend, out):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, dense, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dense, q, backend, out)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    mine = dict(q.get(timeout=5) for _ in range(2))
+    return dict(q.get(timeout=5) for _ in range(world))
+
+
+def test_world2_matches_oracle_jacobi(dense, jacobi_maps):
+    mine = _spawn(2, dense, "gloo", "/VP2")
     assert sorted(mine[0] + mine[1]) == list(range(5)) and mine[0] and mine[1]
     assert _compare(dense + "/VP2", jacobi_maps) == 5 * 4
+
+
+def test_world1_nccl_process_group_matches_oracle_jacobi(dense, jacobi_maps):
+    """A real RCCL process group (world size 1): DepthExchange.gather runs
+    all_gather_into_tensor on device buffers through RCCL after every pass,
+    and the engines borrow the gathered maps (torch/RCCL stream
+    ordering before the borrow)."""
+    mine = _spawn(1, dense, "nccl", "/VPN")
+    assert mine[0] == list(range(5))
+    assert _compare(dense + "/VPN", jacobi_maps) == 5 * 4
+
+
+@pytest.mark.timeout(600)
+def test_world2_multi_scale_matches_oracle_jacobi(tmp_path):
+    """cfg4's schedule (src/main_ACMMP.cpp:96-176) view-parallel: two scales
+    (1010x760 -> 505x380 first), photometric + planar, two geometric passes,
+    JBU, hierarchy + planar, two geometric passes — two ranks on the one GPU
+    against the oracle pipeline in Jacobi order, every .dmb bit-exact."""
+    d = str(tmp_path / "dense_ms")
+    sc = scene.make_scene(num_views=4, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=2)
+    mine = _spawn(2, d, "gloo", "/VPMS")
+    assert sorted(mine[0] + mine[1]) == list(range(4)) and mine[0] and mine[1]
+    maps = OraclePipeline(d).run_multi_scale("jacobi")
+    assert _compare(d + "/VPMS", maps) == 4 * 4
+
+
+def test_bench_under_torchrun_nccl_world1():
+    """bench.py through torch.distributed.run at world size 1: a process
+    group, the RCCL all-gather between the passes, one JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "1", "--warmup", "0", "--width", "400", "--height", "300",
+           "--pmc", "off", "--no-cpu-baseline", "--backend", "nccl"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 1 and res["value"] > 0
+    assert "RCCL all-gather" in res["config"]["parallelism"]
