@@ -1918,6 +1918,10 @@ static int ns_bucket(int nsrc) {
     return 32;
 }
 
+#ifdef ACMMP_DEV_SUBSET  // resource/ISA inspection builds only: one instantiation (NS 9, u8 quads)
+#define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
+#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
+#else
 #define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...)                             \
     switch (ns_bucket(h_kv.nsrc)) {                                                         \
         case 4: KERNEL<4, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;              \
@@ -1939,6 +1943,7 @@ static int ns_bucket(int nsrc) {
         case 4: { ACMMP_LAUNCH_NSW(KERNEL, 4, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         default: { ACMMP_LAUNCH_NSW(KERNEL, 5, GRID, BLOCK, STREAM, __VA_ARGS__) } break;   \
     }
+#endif
 
 static dim3 cs_grid(const KViews &kv, int colours) {
     return dim3((kv.Wh + kBX - 1) / kBX, (kv.H + kBY - 1) / kBY, colours);

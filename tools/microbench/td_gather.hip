@@ -1,0 +1,74 @@
+// TD/TA cost of index-addressed (idxen) dword buffer loads by access pattern
+// on gfx950: the texture-data path that bounds k_sweep. Every
+// wave issues ITERS buffer_load_dword idxen per lane with a pattern-defined
+// record index into a 4-B-record buffer that stays cache resident, and sums
+// the loaded words (kept live through one store). Run under
+//   rocprofv3 --kernel-trace --pmc TD_TD_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE
+// and compare TD busy cycles per wave-instruction per pattern.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+__device__ unsigned sbl32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
+
+constexpr int ITERS = 512;
+constexpr int PITCH = 1632;  // records per row (cfg2 u8-quad pitch)
+
+__global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, int pattern, unsigned *out) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)buf, (short)4, nrec, 0x00020000);
+    const int lane = threadIdx.x & 63, wave = (blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int c = lane & 15, r = lane >> 4;
+    unsigned h = (unsigned)(wave * 2654435761u) ^ (unsigned)lane * 40503u;
+    int base = (wave % 64) * 8 * PITCH + 64;
+    unsigned acc = 0;
+#pragma unroll 1
+    for (int it = 0; it < ITERS; ++it) {
+        int idx;
+        const int s = it & 31;  // 36-sample-like walk: offsets change per iteration
+        switch (pattern) {
+            case 0: idx = base + lane + 64 * (s & 7); break;                            // coalesced 256 B
+            case 1: idx = base + 2 * lane + (s & 7); break;                             // stride 2, one row
+            case 2: idx = base + r * PITCH + 2 * c + (s % 6) * 2 + (s / 6) * 2 * PITCH; break;  // k_sweep wave: 16 cols x 4 rows
+            case 3: {                                                                  // same + per-lane jitter
+                h = h * 1664525u + 1013904223u;
+                idx = base + r * PITCH + 2 * c + (s % 6) * 2 + (s / 6) * 2 * PITCH + (int)((h >> 28) & 3) - 1;
+            } break;
+            case 4: h = h * 1664525u + 1013904223u; idx = (int)(h % (unsigned)nrec); break;  // random
+            case 5: idx = base + (s & 7); break;                                        // broadcast
+            case 6: idx = base + r * PITCH * 2 + 2 * c + (s % 6) * 2; break;            // rows 2 apart
+            default: idx = base + lane * 33; break;                                     // one line per lane
+        }
+        acc += sbl32(rs, idx, 0, 0, 0);
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char **argv) {
+    const int nrec = PITCH * 600;
+    unsigned *buf, *out;
+    (void)hipMalloc(&buf, (size_t)nrec * 4);
+    (void)hipMalloc(&out, 4);
+    (void)hipMemset(buf, 1, (size_t)nrec * 4);
+    const int blocks = 2048;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int p = 0; p < 8; ++p) {
+        for (int rep = 0; rep < 3; ++rep) {
+            (void)hipEventRecord(a);
+            k_gather<<<blocks, 256>>>(buf, nrec, p, out);
+            (void)hipEventRecord(b);
+            (void)hipEventSynchronize(b);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, a, b);
+            if (rep == 2) {
+                const double insts = (double)blocks * 4 * ITERS;
+                printf("pattern %d: %.3f ms, %.2f G wave-inst/s, %.1f ns per inst per CU\n", p, ms,
+                       insts / (ms * 1e-3) / 1e9, ms * 1e6 / (insts / 256));
+            }
+        }
+    }
+    return 0;
+}
