@@ -76,7 +76,6 @@ class Timing(C.Structure):
         ("sweep_launches", C.c_int32),
         ("finalize_ms", C.c_float),
         ("total_ms", C.c_float),
-        ("batch_size", C.c_int32),
     ]
 
 
@@ -174,7 +173,6 @@ SIGNATURES = {
                                                  C.POINTER(C.c_int)]),
     "acmmp_run_patchmatch": (C.c_int, [_CTX]),
     "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
-    "acmmp_run_patchmatch_batch": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
     "acmmp_synchronize": (C.c_int, [_CTX]),
     "acmmp_get_plane_hypotheses": (C.c_int, [_CTX, _FP, C.c_size_t]),
     "acmmp_get_costs": (C.c_int, [_CTX, _FP, C.c_size_t]),

@@ -72,9 +72,6 @@ struct acmmp_ctx {
     acmmp_timing last_timing{};
     hipEvent_t ev[8] = {};
     bool events_made = false;
-    hipEvent_t ev_batch = nullptr;  // cross-stream ordering of batched runs
-    bool timed_run = false;         // the last run's events are this engine's (it led its batch)
-    int batch_size = 0;             // engines in the batch this engine last led
 };
 
 namespace acmmp {
@@ -120,5 +117,6 @@ inline int check_ready(acmmp_ctx *ctx) {
 
 // Builds the KViews constant block for the next enqueue (acmmp_engine.hip).
 int upload_kv(acmmp_ctx *ctx);
+KState make_state(acmmp_ctx *ctx);
 
 }  // namespace acmmp

@@ -122,22 +122,6 @@ int kv_upload(acmmp_ctx *ctx) {
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
     kv.texel = ctx->pad_texel;
-    KBufs &b = kv.buf;
-    for (int c = 0; c < 2; ++c) {
-        for (int k = 0; k < 2; ++k) {
-            b.cplane[c][k] = ctx->d_cplane[c][k];
-            b.ccost[c][k] = ctx->d_ccost[c][k];
-        }
-        b.csv[c] = ctx->d_csv[c];
-    }
-    b.rm_plane = ctx->d_rm_plane;
-    b.rm_cost = ctx->d_rm_cost;
-    b.rm_sv = ctx->d_rm_sv;
-    b.pre_cost = ctx->d_pre_cost;
-    b.prior = ctx->d_prior;
-    b.mask = ctx->d_mask;
-    b.scaled = ctx->d_scaled;
-    b.seed = ctx->d_seed;
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737
@@ -160,6 +144,25 @@ int kv_upload(acmmp_ctx *ctx) {
     return ACMMP_OK;
 }
 
+KState state_of(acmmp_ctx *ctx) {
+    KState st{};
+    for (int c = 0; c < 2; ++c) {
+        st.plane[c] = ctx->d_cplane[c][ctx->cur[c]];
+        st.cost[c] = ctx->d_ccost[c][ctx->cur[c]];
+        st.plane_nx[c] = ctx->d_cplane[c][ctx->cur[c] ^ 1];
+        st.cost_nx[c] = ctx->d_ccost[c][ctx->cur[c] ^ 1];
+        st.sv[c] = ctx->d_csv[c];
+    }
+    st.rm_plane = ctx->d_rm_plane;
+    st.rm_cost = ctx->d_rm_cost;
+    st.rm_sv = ctx->d_rm_sv;
+    st.pre_cost = ctx->d_pre_cost;
+    st.prior = ctx->d_prior;
+    st.mask = ctx->d_mask;
+    st.scaled = ctx->d_scaled;
+    st.seed = ctx->d_seed;
+    return st;
+}
 
 
 int upload_pitched(acmmp_ctx *ctx, float *&dst, int &pitch, const float *src, int w, int h, bool device_src) {
@@ -342,19 +345,6 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
     return ACMMP_OK;
 }
 
-// Template bucket of the engine's kernels (same key: one batch may hold both).
-int batch_key_of(const acmmp_ctx *ctx) {
-    KViews k{};
-    k.nsrc = ctx->n - 1;
-    k.texel = ctx->pad_texel;
-    k.wide = 0;
-    for (int i = 1; i < ctx->n; ++i)
-        if ((size_t)ctx->pad_pitch[i] * (ctx->cams[i].height + 2) >= (1u << 24)) k.wide = 1;
-    if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
-        if (e[0] == '1') k.wide = 1;
-    return batch_key(k);
-}
-
 float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.f;
@@ -365,6 +355,7 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 
 namespace acmmp {
 int upload_kv(acmmp_ctx *ctx) { return kv_upload(ctx); }
+KState make_state(acmmp_ctx *ctx) { return state_of(ctx); }
 }  // namespace acmmp
 
 extern "C" {
@@ -438,7 +429,6 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     }
     if (ctx->events_made)
         for (auto &e : ctx->ev) (void)hipEventDestroy(e);
-    if (ctx->ev_batch) (void)hipEventDestroy(ctx->ev_batch);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -603,8 +593,7 @@ int acmmp_set_planar_prior(acmmp_ctx *ctx, const float *plane_params4, int num_p
     return ACMMP_OK;
 }
 
-// Preconditions of a run (the inputs its flags need).
-static int run_ready(acmmp_ctx *ctx) {
+int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     int rc = check_ready(ctx);
     if (rc) return rc;
     const acmmp_params &p = ctx->prm;
@@ -618,115 +607,44 @@ static int run_ready(acmmp_ctx *ctx) {
     if (p.patch_size != 11 || p.radius_increment != 2)
         return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "only patch_size 11 / radius_increment 2 are built");
     if (p.max_iterations < 0) return set_err(ctx, ACMMP_ERR_ARG, "max_iterations < 0");
-    return ACMMP_OK;
-}
-
-// Enqueues RunPatchMatch for n <= kMaxBatch engines that share one kernel
-// instantiation, device and iteration count as ONE launch per stage on the
-// first engine's stream: that stream waits for the others' queued work
-// (their constants and state uploads), and their streams wait for the batch.
-static int run_group(acmmp_ctx *const *ctxs, int n) {
-    acmmp_ctx *lead = ctxs[0];
-    HIP_TRY(lead, hipSetDevice(lead->device));
-    BatchDesc bd{};
-    bd.n = n;
-    for (int i = 0; i < n; ++i) {
-        acmmp_ctx *c = ctxs[i];
-        const int rc = kv_upload(c);
-        if (rc) return rc;
-        bd.d_kv[i] = c->d_kv;
-        bd.h_kv[i] = &c->h_kv;
-        if (!c->ev_batch) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_batch, hipEventDisableTiming));
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    rc = kv_upload(ctx);
+    if (rc) return rc;
+    if (ctx->timing && !ctx->events_made) {
+        for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
+        ctx->events_made = true;
     }
-    hipStream_t s = lead->stream;
-    for (int i = 1; i < n; ++i) {
-        HIP_TRY(ctxs[i], hipEventRecord(ctxs[i]->ev_batch, ctxs[i]->stream));
-        HIP_TRY(lead, hipStreamWaitEvent(s, ctxs[i]->ev_batch, 0));
-    }
-    if (lead->timing && !lead->events_made) {
-        for (auto &e : lead->ev) HIP_TRY(lead, hipEventCreate(&e));
-        lead->events_made = true;
-    }
-    const int iters = lead->prm.max_iterations;
-    if (lead->timing) HIP_TRY(lead, hipEventRecord(lead->ev[0], s));
-    HIP_TRY(lead, launch_init(bd, s));
-    if (lead->timing) HIP_TRY(lead, hipEventRecord(lead->ev[1], s));
-    for (int it = 0; it < iters; ++it)
-        for (int colour = 0; colour < 2; ++colour)  // BlackPixelUpdate, RedPixelUpdate
-            HIP_TRY(lead, launch_sweep(bd, colour, it, s));
-    if (lead->timing) HIP_TRY(lead, hipEventRecord(lead->ev[2], s));
-    HIP_TRY(lead, launch_finalize(bd, iters, s));
-    HIP_TRY(lead, launch_filter(bd, 0, s));
-    HIP_TRY(lead, launch_filter(bd, 1, s));
-    if (lead->timing) HIP_TRY(lead, hipEventRecord(lead->ev[3], s));
-    if (n > 1) {
-        HIP_TRY(lead, hipEventRecord(lead->ev_batch, s));
-        for (int i = 1; i < n; ++i) HIP_TRY(ctxs[i], hipStreamWaitEvent(ctxs[i]->stream, lead->ev_batch, 0));
-    }
-    for (int i = 0; i < n; ++i) {
-        acmmp_ctx *c = ctxs[i];
-        c->cur[0] = c->cur[1] = iters & 1;
-        c->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
-        c->have_state = true;
-        c->timed_run = (i == 0) && c->timing;
-        c->batch_size = (i == 0) ? n : 0;
-    }
-    return ACMMP_OK;
-}
-
-static int run_batch(acmmp_ctx *const *ctxs, int n) {
-    if (!ctxs || n < 1) return ACMMP_ERR_ARG;
-    for (int i = 0; i < n; ++i) {
-        if (!ctxs[i]) return ACMMP_ERR_ARG;
-        for (int k = 0; k < i; ++k)
-            if (ctxs[k] == ctxs[i]) return set_err(ctxs[i], ACMMP_ERR_ARG, "engine %d appears twice in the batch", i);
-        const int rc = run_ready(ctxs[i]);
-        if (rc) return rc;
-    }
-    // greedy groups of compatible engines, in order
-    std::vector<bool> done(n, false);
-    for (int i = 0; i < n; ++i) {
-        if (done[i]) continue;
-        acmmp_ctx *group[kMaxBatch];
-        int m = 0;
-        group[m++] = ctxs[i];
-        done[i] = true;
-        const int key = batch_key_of(ctxs[i]);
-        for (int k = i + 1; k < n && m < kMaxBatch; ++k) {
-            if (done[k] || ctxs[k]->device != ctxs[i]->device || batch_key_of(ctxs[k]) != key ||
-                ctxs[k]->prm.max_iterations != ctxs[i]->prm.max_iterations)
-                continue;
-            group[m++] = ctxs[k];
-            done[k] = true;
+    hipStream_t s = ctx->stream;
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
+    ctx->cur[0] = ctx->cur[1] = 0;
+    HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
+    for (int it = 0; it < p.max_iterations; ++it) {
+        for (int colour = 0; colour < 2; ++colour) {  // BlackPixelUpdate, RedPixelUpdate
+            HIP_TRY(ctx, launch_sweep(ctx->d_kv, ctx->h_kv, state_of(ctx), colour, it, s));
+            ctx->cur[colour] ^= 1;
         }
-        const int rc = run_group(group, m);
-        if (rc) return rc;
     }
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
+    HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 0, s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 1, s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
+    ctx->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
+    ctx->have_state = true;
     return ACMMP_OK;
 }
-
-int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
-    acmmp_ctx *one[1] = {ctx};
-    return run_batch(one, 1);
-}
-
-int acmmp_run_patchmatch_batch(acmmp_ctx *const *ctxs, int n) { return run_batch(ctxs, n); }
 
 int acmmp_synchronize(acmmp_ctx *ctx) {
     if (!ctx) return ACMMP_ERR_ARG;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->timing && ctx->events_made && ctx->timed_run) {
-        // the events of the batch this engine led (a batch member that did
-        // not lead reports no launches of its own)
+    if (ctx->timing && ctx->events_made) {
         acmmp_timing &t = ctx->last_timing;
         t.init_ms = elapsed(ctx->ev[0], ctx->ev[1]);
         t.sweep_ms = elapsed(ctx->ev[1], ctx->ev[2]);
         t.sweep_launches = 2 * ctx->prm.max_iterations;
         t.finalize_ms = elapsed(ctx->ev[2], ctx->ev[3]);
         t.total_ms = elapsed(ctx->ev[0], ctx->ev[3]);
-        t.batch_size = ctx->batch_size;
-    } else if (ctx->timing) {
-        ctx->last_timing = acmmp_timing{};
     }
     return ACMMP_OK;
 }

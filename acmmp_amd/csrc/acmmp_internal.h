@@ -33,24 +33,7 @@ struct ViewRel {
 // Texel forms of the padded source views (KViews::texel).
 enum { kTexelF32 = 0, kTexelU8 = 1, kTexelH16 = 2 };
 
-// Device buffers of one engine's PatchMatch state (acmmp_ctx), carried in
-// its KViews so that one launch can serve several engines (KBatch).
-struct KBufs {
-    float4 *cplane[2][2];   // colour-split planes [colour][ping-pong]
-    float *ccost[2][2];
-    uint32_t *csv[2];       // colour-split selected views (in place)
-    float4 *rm_plane;       // row-major state between runs
-    float *rm_cost;
-    uint32_t *rm_sv;
-    float *pre_cost;        // hierarchy (row-major)
-    const float4 *prior;    // planar prior planes (row-major)
-    const uint32_t *mask;   // planar prior triangle labels
-    const float4 *scaled;   // hierarchy low-res planes (scaled_rows x scaled_cols)
-    const float4 *seed;     // seeded priors
-};
-
 struct KViews {
-    KBufs buf;
     acmmp_params prm;
     acmmp_camera cam[ACMMP_MAX_IMAGES];
     ViewRel rel[ACMMP_MAX_IMAGES];            // rel[v] for source v (1-based), rel[0] unused
@@ -97,38 +80,14 @@ struct KState {
     const float4 *seed;     // seeded priors
 };
 
-// Several independent problems (one reference view / engine each) in ONE
-// launch per stage: the 1-D grid is the concatenation of the problems' block
-// ranges [start[i], start[i + 1]), gx[i] blocks per block row, gy[i] rows. The problems
-// of a batch share the kernels' template parameters (source-view bucket and
-// texel form) and the iteration count. A launch that fills the chip once
-// instead of leaving the tail of one view's last block round idle.
-constexpr int kMaxBatch = 4;
-struct KBatch {
-    const KViews *kv[kMaxBatch];
-    int start[kMaxBatch + 1];
-    int gx[kMaxBatch], gy[kMaxBatch];
-    int n;
-};
-
-// Host description of a batch: device and host copies of each problem's
-// KViews (the host copy gives sizes and the template choice).
-struct BatchDesc {
-    const KViews *d_kv[kMaxBatch];
-    const KViews *h_kv[kMaxBatch];
-    int n;
-};
-
 // Kernel launchers (acmmp_kernels.hip). All enqueue on `stream`.
-// Ping-pong phases follow from the launch order: the sweep of (iter,
-// colour) reads plane[0] = cplane[0][(iter + colour) & 1] and plane[1] =
-// cplane[1][iter & 1]; finalize reads cplane[c][iters & 1].
-hipError_t launch_init(const BatchDesc &b, hipStream_t stream);
-hipError_t launch_sweep(const BatchDesc &b, int colour, int iter, hipStream_t stream);
-hipError_t launch_finalize(const BatchDesc &b, int iters, hipStream_t stream);
-hipError_t launch_filter(const BatchDesc &b, int colour, hipStream_t stream);
-// the template bucket of a problem (same value = one batch may hold both)
-int batch_key(const KViews &h_kv);
+hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream);
+hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                        int iter, hipStream_t stream);
+hipError_t launch_finalize(const KViews *d_kv, const KViews &h_kv, const KState &st,
+                           hipStream_t stream);
+hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                         hipStream_t stream);
 hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float4 *planes,
                              float *out_costs, float *out_init, uint32_t *out_views,
                              hipStream_t stream);

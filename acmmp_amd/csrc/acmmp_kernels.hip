@@ -936,82 +936,16 @@ DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
 
 DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, threadIdx.y * kBX + threadIdx.x); }
 
-// ------------------------------------------------------- batched launches
-// One launch serves kb.n problems (KBatch): the 1-D grid is first put in the
-// XCD-aware order of xcd_block (each XCD walks one contiguous run of
-// blocks, so it works on one band of one problem at a time), then the
-// problem whose block range holds the block is found (<= 4 compares on
-// kernel arguments, no memory), and its KViews is read through the scalar
-// cache as in the single-problem case.
-DEV int pick4(int b, int a0, int a1, int a2, int a3) { return b == 0 ? a0 : b == 1 ? a1 : b == 2 ? a2 : a3; }
-
-struct BatchBlock {
-    const KViews *kv;
-    int local;   // block index inside its problem
-    int gx, gy;  // that problem's blocks per row / rows of blocks
-};
-
-DEV BatchBlock batch_block(const KBatch &kb) {
-    const int T = gridDim.x, L = blockIdx.x;
-    const int xcd = L & 7, i = L >> 3, q = T >> 3, r = T & 7;
-    const int nl = (xcd < r) ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
-    int b = 0;
-    if (kb.n > 1 && nl >= kb.start[1]) b = 1;
-    if (kb.n > 2 && nl >= kb.start[2]) b = 2;
-    if (kb.n > 3 && nl >= kb.start[3]) b = 3;
-    BatchBlock o;
-    o.kv = b == 0 ? kb.kv[0] : b == 1 ? kb.kv[1] : b == 2 ? kb.kv[2] : kb.kv[3];
-    o.local = nl - pick4(b, kb.start[0], kb.start[1], kb.start[2], kb.start[3]);
-    o.gx = pick4(b, kb.gx[0], kb.gx[1], kb.gx[2], kb.gx[3]);
-    o.gy = pick4(b, kb.gy[0], kb.gy[1], kb.gy[2], kb.gy[3]);
-    return o;
-}
-
-DEV BlockXY block_xy(int local, int gx) {
-    BlockXY b;
-    b.by = local / gx;
-    b.bx = local - b.by * gx;
-    return b;
-}
-
-// The state buffers a launch reads and writes: plane[c] = cplane[c][cur_c]
-// (current), plane_nx[c] = the other ping-pong buffer (acmmp_internal.h).
-DEV KState state_at(const KViews &kv, int cur0, int cur1) {
-    KState st;
-    st.plane[0] = kv.buf.cplane[0][cur0];
-    st.plane_nx[0] = kv.buf.cplane[0][cur0 ^ 1];
-    st.cost[0] = kv.buf.ccost[0][cur0];
-    st.cost_nx[0] = kv.buf.ccost[0][cur0 ^ 1];
-    st.plane[1] = kv.buf.cplane[1][cur1];
-    st.plane_nx[1] = kv.buf.cplane[1][cur1 ^ 1];
-    st.cost[1] = kv.buf.ccost[1][cur1];
-    st.cost_nx[1] = kv.buf.ccost[1][cur1 ^ 1];
-    st.sv[0] = kv.buf.csv[0];
-    st.sv[1] = kv.buf.csv[1];
-    st.rm_plane = kv.buf.rm_plane;
-    st.rm_cost = kv.buf.rm_cost;
-    st.rm_sv = kv.buf.rm_sv;
-    st.pre_cost = kv.buf.pre_cost;
-    st.prior = kv.buf.prior;
-    st.mask = kv.buf.mask;
-    st.scaled = kv.buf.scaled;
-    st.seed = kv.buf.seed;
-    return st;
-}
-
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
 // writes the colour-split "current" buffers. blockIdx.z = colour.
 template <int NS, int TX>
-__global__ __launch_bounds__(256) void k_init(KBatch kb) {
+__global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
-    const BatchBlock bb = batch_block(kb);
-    const KViews &kv = *bb.kv;
-    const int per = bb.gx * bb.gy;  // blocks per colour
-    const int colour = bb.local >= per ? 1 : 0;
-    const BlockXY blk = block_xy(bb.local - colour * per, bb.gx);
-    const KState st = state_at(kv, 0, 0);
+    const KViews &kv = *kvp;
+    const int colour = blockIdx.z;
+    const BlockXY blk = xcd_block();
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
@@ -1190,17 +1124,16 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
 // half-sweep snapshot); own state lives in registers and is written to the
 // "next" buffer of this colour.
 template <int NS, int TX>
-__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(KBatch kb, int colour, int iter) {
+__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
+                                                  int iter) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
 #if ACMMP_CAND_LDS
     __shared__ float4 cand_lds[8 * kThreads];
 #endif
     DIAG_T(t_start);
-    const BatchBlock bb = batch_block(kb);
-    const KViews &kv = *bb.kv;
-    const BlockXY blk = block_xy(bb.local, bb.gx);
-    const KState st = state_at(kv, (iter + colour) & 1, iter & 1);
+    const KViews &kv = *kvp;
+    const BlockXY blk = xcd_block();
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
@@ -1703,13 +1636,10 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(KBatch kb, int
     DIAG_ADD(4, t_select, t_end);
 }
 
-__global__ __launch_bounds__(256) void k_finalize(KBatch kb, int iters) {
-    const BatchBlock bb = batch_block(kb);
-    const KViews &kv = *bb.kv;
-    const BlockXY blk = block_xy(bb.local, bb.gx);
-    const KState st = state_at(kv, iters & 1, iters & 1);
-    const int px = blk.bx * 64 + threadIdx.x;
-    const int py = blk.by * 4 + threadIdx.y;
+__global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
+    const KViews &kv = *kvp;
+    const int px = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
     if (px >= kv.W || py >= kv.H) return;
     const int c = (px + py) & 1;
     const int ci = cs_index(kv, px, py);
@@ -1724,19 +1654,17 @@ __global__ __launch_bounds__(256) void k_finalize(KBatch kb, int iters) {
 
 // CheckerboardFilter (src/ACMMP.cu:1214-1328) on one colour, in place on the
 // row-major planes: every read is of the opposite colour.
-__global__ __launch_bounds__(256) void k_filter(KBatch kb, int colour) {
-    const BatchBlock bb = batch_block(kb);
-    const KViews &kv = *bb.kv;
-    const BlockXY blk = block_xy(bb.local, bb.gx);
-    const int k = blk.bx * 64 + threadIdx.x;
-    const int py = blk.by * 4 + threadIdx.y;
+__global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, KState st, int colour) {
+    const KViews &kv = *kvp;
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    const int py = blockIdx.y * 4 + threadIdx.y;
     const int width = kv.W, height = kv.H;
     if (py >= kv.sweep_rows) return;
     const int px = 2 * k + ((py + colour) & 1);
     if (px >= width) return;
-    float4 *ph = kv.buf.rm_plane;
+    float4 *ph = st.rm_plane;
     const int center = py * width + px;
-    if (kv.buf.rm_cost[center] < 0.001f) return;
+    if (st.rm_cost[center] < 0.001f) return;
     float f[21];
     int n = 0;
     f[n++] = ph[center].w;
@@ -2021,64 +1949,27 @@ static dim3 cs_grid(const KViews &kv, int colours) {
     return dim3((kv.Wh + kBX - 1) / kBX, (kv.H + kBY - 1) / kBY, colours);
 }
 
-// KBatch of a launch whose problem i has gx(i) x gy(i) blocks, `mult` such
-// grids (colours) each.
-template <typename GX, typename GY>
-static KBatch make_batch(const BatchDesc &b, GX gx, GY gy, int mult, int &total) {
-    KBatch kb{};
-    kb.n = b.n;
-    total = 0;
-    for (int i = 0; i < b.n; ++i) {
-        kb.kv[i] = b.d_kv[i];
-        kb.gx[i] = gx(*b.h_kv[i]);
-        kb.gy[i] = gy(*b.h_kv[i]);
-        kb.start[i] = total;
-        total += mult * kb.gx[i] * kb.gy[i];
-    }
-    for (int i = b.n; i < kMaxBatch; ++i) {
-        kb.kv[i] = b.d_kv[0];
-        kb.start[i] = total;
-        kb.gx[i] = kb.gy[i] = 1;
-    }
-    kb.start[kMaxBatch] = total;
-    return kb;
-}
-
-static int cs_gx(const KViews &v) { return (v.Wh + kBX - 1) / kBX; }
-static int rm_gx(const KViews &v) { return (v.W + 63) / 64; }
-static int row_gy(const KViews &v) { return (v.H + kBY - 1) / kBY; }
-
-int batch_key(const KViews &h_kv) {
-    return ns_bucket(h_kv.nsrc) * 16 + (h_kv.wide ? 1 : 0) * 4 + h_kv.texel;
-}
-
-hipError_t launch_init(const BatchDesc &b, hipStream_t stream) {
-    int total = 0;
-    const KBatch kb = make_batch(b, cs_gx, row_gy, 2, total);
-    const KViews &h_kv = *b.h_kv[0];
-    ACMMP_LAUNCH_NS(k_init, dim3(total), dim3(kBX, kBY), stream, kb);
+hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
+    ACMMP_LAUNCH_NS(k_init, cs_grid(h_kv, 2), dim3(kBX, kBY), stream, d_kv, st);
     return hipGetLastError();
 }
 
-hipError_t launch_sweep(const BatchDesc &b, int colour, int iter, hipStream_t stream) {
-    int total = 0;
-    const KBatch kb = make_batch(b, cs_gx, row_gy, 1, total);
-    const KViews &h_kv = *b.h_kv[0];
-    ACMMP_LAUNCH_NS(k_sweep, dim3(total), dim3(kBX, kBY), stream, kb, colour, iter);
+hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
+                        hipStream_t stream) {
+    ACMMP_LAUNCH_NS(k_sweep, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
     return hipGetLastError();
 }
 
-hipError_t launch_finalize(const BatchDesc &b, int iters, hipStream_t stream) {
-    int total = 0;
-    const KBatch kb = make_batch(b, rm_gx, row_gy, 1, total);
-    k_finalize<<<dim3(total), dim3(64, 4), 0, stream>>>(kb, iters);
+hipError_t launch_finalize(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
+    k_finalize<<<grid, block, 0, stream>>>(d_kv, st);
     return hipGetLastError();
 }
 
-hipError_t launch_filter(const BatchDesc &b, int colour, hipStream_t stream) {
-    int total = 0;
-    const KBatch kb = make_batch(b, cs_gx, row_gy, 1, total);
-    k_filter<<<dim3(total), dim3(64, 4), 0, stream>>>(kb, colour);
+hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
+                         hipStream_t stream) {
+    dim3 block(64, 4), grid((h_kv.Wh + 63) / 64, (h_kv.H + 3) / 4);
+    k_filter<<<grid, block, 0, stream>>>(d_kv, st, colour);
     return hipGetLastError();
 }
 

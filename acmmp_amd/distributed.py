@@ -135,12 +135,11 @@ def _view_params(t: ViewTask) -> _abi.Params:
     return p
 
 
-def engine_compute(t: ViewTask, eng: ACMMP):
+def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
     """ProcessProblem's per-view work (src/acmmp_definitions.cpp:260-379) on
-    a pooled engine, as an EnginePool generator (each yield = one run):
-    images, previous state and source depth maps borrowed from HBM, results
-    exported device-to-device into fresh tensors (the previous pass's
-    tensors may still be read by the .dmb writers). Returns a ViewResult."""
+    a pooled engine: images, previous state and source depth maps borrowed
+    from HBM, results exported device-to-device into fresh tensors (the
+    previous pass's tensors may still be read by the .dmb writers)."""
     ref = t.images[0]
     H, W = ref.shape
     planes = torch.empty((H, W, 4), dtype=torch.float32, device=ref.device)
@@ -152,11 +151,11 @@ def engine_compute(t: ViewTask, eng: ACMMP):
         eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
     if t.hierarchy:
         eng.set_hierarchy_inputs(*t.hier_inputs)
-    yield  # the run (batched with the pass's other views by the pool)
+    eng.run_async()
     if t.planar:
         eng.synchronize()
         eng.prepare_planar_prior()
-        yield  # the planar-prior run
+        eng.run_async()
     eng.export_results(planes.data_ptr(), costs.data_ptr(), 0)
     eng.synchronize()
     return ViewResult(planes, costs)

@@ -276,20 +276,6 @@ class ACMMP:
     def run_async(self):
         self._check(self._lib.acmmp_run_patchmatch_async(self._ctx), "acmmp_run_patchmatch_async")
 
-    @staticmethod
-    def run_batch(engines: Sequence["ACMMP"]):
-        """RunPatchMatch of several engines (views) sharing each launch
-        (acmmp_run_patchmatch_batch); asynchronous like run_async."""
-        if not engines:
-            return
-        lib = engines[0]._lib
-        arr = (C.c_void_p * len(engines))(*[e._ctx.value for e in engines])
-        rc = lib.acmmp_run_patchmatch_batch(arr, len(engines))
-        if rc != _abi.OK:
-            msgs = [lib.acmmp_last_error(e._ctx) for e in engines]
-            raise AcmmpError(f"acmmp_run_patchmatch_batch: status {rc}: "
-                             + "; ".join(m.decode() for m in msgs if m))
-
     def synchronize(self):
         self._check(self._lib.acmmp_synchronize(self._ctx), "acmmp_synchronize")
 

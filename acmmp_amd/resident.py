@@ -5,10 +5,10 @@ HBM.
 This is the schedule `bench.py` times and the view-parallel driver
 (`distributed.py`) uses:
 
-* `EnginePool` owns S engines and runs S views at a time through ONE launch
-  per stage (acmmp_run_patchmatch_batch), so a launch fills the chip instead
-  of leaving the tail of one view's last block round idle (or, mode
-  "streams", one host thread per engine and stream).
+* `EnginePool` owns S engines. One host thread per engine takes the next view
+  of the pass off a shared queue as soon as its previous view finished (the
+  library's ctypes calls release the GIL), so S views are in flight and the
+  tail of one view's sweep launch fills with another's blocks.
 * `photometric_view` / `geometric_view` are one view's RunPatchMatch
   (src/ACMMP.cu:1378-1456) with images borrowed from HBM
   (`acmmp_set_images_device`), the previous pass's state and the gathered
@@ -33,24 +33,11 @@ from .engine import ACMMP
 
 
 class EnginePool:
-    """S engines on one device. `map(fn, jobs)` runs fn(engine, job) for
-    every job and returns the results in job order. fn is a generator
-    function: it prepares its engine (parameters, borrowed inputs), yields,
-    and after the run exports and finishes (see photometric_view).
+    """S engines on one device. `map(fn, jobs)` calls fn(engine, job) for
+    every job, S at a time, and returns the results in job order."""
 
-    mode "batch" (default): S views at a time share every launch
-    (acmmp_run_patchmatch_batch) on one stream — a launch of S views fills
-    the chip instead of leaving the tail of one view's last block round idle,
-    and one kernel's duration is one launch's.
-    mode "streams": one host thread per engine takes the next view off a
-    shared queue and runs it on the engine's own stream (S views' launches
-    overlap on the GPU)."""
-
-    def __init__(self, device: int, streams: int = 2, timing: bool = False, mode: str = "batch"):
-        if mode not in ("batch", "streams"):
-            raise ValueError(f"mode {mode!r}")
+    def __init__(self, device: int, streams: int = 2, timing: bool = False):
         self.device = device
-        self.mode = mode
         self.engines = [ACMMP(device) for _ in range(max(int(streams), 1))]
         for e in self.engines:
             e.set_timing(timing)
@@ -58,7 +45,6 @@ class EnginePool:
         self._lock = threading.Lock()
         self.sweep_ms = 0.0
         self.sweep_launches = 0
-        self.batches = 0
 
     def __len__(self):
         return len(self.engines)
@@ -76,61 +62,23 @@ class EnginePool:
 
     def reset_timing(self):
         with self._lock:
-            self.sweep_ms, self.sweep_launches, self.batches = 0.0, 0, 0
+            self.sweep_ms, self.sweep_launches = 0.0, 0
 
     def finish(self, eng: ACMMP):
-        """Waits for the engine's stream; accumulates the sweep timing of the
-        launches it led."""
+        """Waits for the engine's stream; accumulates its sweep timing."""
         eng.synchronize()
         if self.timing:
             t = eng.timing()
             with self._lock:
                 self.sweep_ms += t["sweep_ms"]
                 self.sweep_launches += t["sweep_launches"]
-                self.batches += 1 if t["sweep_launches"] else 0
-
-    def run_one(self, fn, job, eng: ACMMP | None = None):
-        """One view on one engine: every yield of its generator is one run."""
-        eng = eng or self.engines[0]
-        g = fn(eng, job)
-        try:
-            next(g)
-            while True:
-                eng.run_async()
-                next(g)
-        except StopIteration as stop:
-            return stop.value
 
     def map(self, fn: Callable, jobs: Sequence):
         jobs = list(jobs)
         results = [None] * len(jobs)
-        S = len(self.engines)
-        if self.mode == "batch":
-            # each round runs the views whose generators yielded (a view may
-            # run more than once, e.g. the planar-prior pass) as one batch
-            for base in range(0, len(jobs), S):
-                active = []
-                for e, k in zip(self.engines, range(base, min(base + S, len(jobs)))):
-                    g = fn(e, jobs[k])
-                    try:
-                        next(g)
-                        active.append((e, g, k))
-                    except StopIteration as stop:
-                        results[k] = stop.value
-                while active:
-                    ACMMP.run_batch([e for e, _, _ in active])
-                    still = []
-                    for e, g, k in active:
-                        try:
-                            next(g)
-                            still.append((e, g, k))
-                        except StopIteration as stop:
-                            results[k] = stop.value
-                    active = still
-            return results
-        if S == 1 or len(jobs) <= 1:
+        if len(self.engines) == 1 or len(jobs) <= 1:
             for k, job in enumerate(jobs):
-                results[k] = self.run_one(fn, job)
+                results[k] = fn(self.engines[0], job)
             return results
         queue = list(range(len(jobs)))
         errors = []
@@ -142,7 +90,7 @@ class EnginePool:
                         if not queue or errors:
                             return
                         k = queue.pop(0)
-                    results[k] = self.run_one(fn, jobs[k], eng)
+                    results[k] = fn(eng, jobs[k])
             except BaseException as e:  # re-raised on the calling thread
                 with self._lock:
                     errors.append(e)
@@ -159,14 +107,14 @@ class EnginePool:
 
 def photometric_view(pool: EnginePool, eng: ACMMP, params: _abi.Params, cams: Sequence[_abi.Camera],
                      image_ptrs: Sequence[int], planes_out: int, costs_out: int, depth_out: int = 0,
-                     pitches: Optional[Sequence[int]] = None):
-    """Photometric RunPatchMatch of one view (generator, see EnginePool);
-    results exported to device buffers (planes (H,W,4), costs (H,W), depth
-    (H,W) = planes[..., 3]). Returns the parameters the run used."""
+                     pitches: Optional[Sequence[int]] = None) -> _abi.Params:
+    """Photometric RunPatchMatch of one view; results exported to device
+    buffers (planes (H,W,4), costs (H,W), depth (H,W) = planes[..., 3]).
+    Returns the parameters the run used (for the oracle)."""
     eng.set_params(params)
     eng.set_images_device(cams, image_ptrs, pitches)
     used = eng.params
-    yield
+    eng.run_async()
     eng.export_results(planes_out, costs_out, depth_out)
     pool.finish(eng)
     return used
@@ -176,18 +124,17 @@ def geometric_view(pool: EnginePool, eng: ACMMP, params: _abi.Params, cams: Sequ
                    image_ptrs: Sequence[int], depth_ptrs: Sequence[int], planes: int, costs: int,
                    planes_out: int = 0, costs_out: int = 0, depth_out: int = 0,
                    pitches: Optional[Sequence[int]] = None,
-                   depth_pitches: Optional[Sequence[int]] = None):
-    """Geometric-consistency RunPatchMatch of one view (generator) from the
-    previous pass's state (planes/costs, device) and the source depth maps
-    (device, e.g. slices of an all-gather). `params` must carry
-    geom_consistency and the pass's max_iterations. Outputs default to
-    overwriting the inputs."""
+                   depth_pitches: Optional[Sequence[int]] = None) -> _abi.Params:
+    """Geometric-consistency RunPatchMatch of one view from the previous
+    pass's state (planes/costs, device) and the source depth maps (device,
+    e.g. slices of an all-gather). `params` must carry geom_consistency and
+    the pass's max_iterations. Outputs default to overwriting the inputs."""
     eng.set_params(params)
     eng.set_images_device(cams, image_ptrs, pitches)
     eng.set_depth_maps_device(depth_ptrs, depth_pitches)
     eng.set_plane_hypotheses_device(planes, costs)
     used = eng.params
-    yield
+    eng.run_async()
     eng.export_results(planes_out or planes, costs_out or costs, depth_out)
     pool.finish(eng)
     return used
@@ -230,7 +177,7 @@ class ResidentViews:
         def one(eng, kv):
             k, v = kv
             ids = self._ids(v)
-            self.used_params[("photo", v)] = yield from photometric_view(
+            self.used_params[("photo", v)] = photometric_view(
                 self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
                 self.planes[k].data_ptr(), self.costs[k].data_ptr(), self.my_depth[k].data_ptr())
         self.pool.map(one, list(enumerate(self.mine)))
@@ -242,7 +189,7 @@ class ResidentViews:
         def one(eng, kv):
             k, v = kv
             ids = self._ids(v)
-            self.used_params[("geom", v)] = yield from geometric_view(
+            self.used_params[("geom", v)] = geometric_view(
                 self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
                 [self.all_depth[self._depth_index(i)].data_ptr() for i in ids],
                 self.planes[k].data_ptr(), self.costs[k].data_ptr())

@@ -63,9 +63,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="800x600", help="ref-view crop timed on the CPU oracle")
     ap.add_argument("--streams", type=int, default=2,
-                    help="views per GPU in flight: per launch (--mode batch) or on their own HIP streams")
-    ap.add_argument("--mode", default="batch", choices=["batch", "streams"],
-                    help="batch: S views share every launch on one stream; streams: S engines on S streams")
+                    help="engines (HIP streams) per GPU running different views concurrently")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to test on one GPU)")
     ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
@@ -141,7 +139,7 @@ def main():
     torch.cuda.synchronize()
 
     n_img = 1 + args.nsrc
-    pool = EnginePool(dev_index, streams, timing=True, mode=args.mode)
+    pool = EnginePool(dev_index, streams, timing=True)
     rv = ResidentViews(pool, cams, images, srcs, mine, H, W, total_views=V if distributed else None)
     all_depth = rv.all_depth
     photo_params = default_params()
@@ -183,7 +181,6 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     timed_ms, timed_launches = pool.sweep_ms, pool.sweep_launches
-    view_launches = 2 * args.iters * 2 * args.views * args.steps  # k_sweep launches of one view, all views, both passes
     if args.pmc_child:
         pool.close()
         return
@@ -192,14 +189,13 @@ def main():
     # un-overlapped duration of a k_sweep launch (HIP events on the engine's
     # stream), the denominator of the roofline fractions
     iso_pool = EnginePool(dev_index, 1, timing=True)
+    eng = iso_pool.engines[0]
     k0, v0 = work[0]
     ids0 = [v0] + srcs[v0]
-    iso_pool.run_one(lambda eng, _: photometric_view(
-        iso_pool, eng, photo_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
-        rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr(), rv.my_depth[k0].data_ptr()), None)
-    iso_pool.run_one(lambda eng, _: geometric_view(
-        iso_pool, eng, geom_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
-        [all_depth[i].data_ptr() for i in ids0], rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr()), None)
+    photometric_view(iso_pool, eng, photo_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
+                     rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr(), rv.my_depth[k0].data_ptr())
+    geometric_view(iso_pool, eng, geom_params, [cams[i] for i in ids0], [images[i].data_ptr() for i in ids0],
+                   [all_depth[i].data_ptr() for i in ids0], rv.planes[k0].data_ptr(), rv.costs[k0].data_ptr())
     iso_ms = iso_pool.sweep_ms / max(iso_pool.sweep_launches, 1)
     iso_pool.close()
 
@@ -230,15 +226,14 @@ def main():
             "iters": args.iters,
             "parallelism": f"view-parallel x{world} (one process per GPU, "
                            f"{('RCCL' if backend == 'nccl' else 'gloo') if distributed else 'no'} "
-                           f"all-gather of depth maps between the passes; "
-                           + (f"{streams} views per launch, one stream)" if args.mode == "batch" else
-                              f"{streams} views in flight per GPU on {streams} HIP streams)"),
+                           f"all-gather of depth maps between the passes; {streams} views in flight per GPU on "
+                           f"{streams} HIP streams)",
             "value_counts": "RunPatchMatch pixels (2 passes per view); per reference view (photometric + "
                             f"geometric) = {value / 2:.2f} Mpix/s",
             "residency": "images, state and depth maps stay in HBM; results exported device-to-device "
                          "(no per-run D2H copy as in the reference's RunPatchMatch, src/ACMMP.cu:1453-1454)",
         },
-        "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, view_launches, streams, args.mode),
+        "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, streams),
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -250,62 +245,56 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, view_launches, streams, mode):
+def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
     """The dominant kernel's roofline (k_sweep, >90 % of the step's GPU time).
 
     k_sweep is bound by the texture-data (TD) path that serves its
     buffer_load gathers, so the binding roofline is that
-    unit's: achieved = gather wave-instructions per second over the timed
-    region's k_sweep launches (HIP events on the launching stream), peak =
-    the rate at which the TD would be 100 % busy at the measured TD cycles
-    per instruction (256 CUs x clock / cycles per instruction), frac =
-    achieved / peak. Per-view counts come from the counter passes (one view
-    per launch); `views_per_launch` views share each timed launch. The HBM
-    roofline is reported beside it from the memory-side counter bytes."""
-    batched = mode == "batch"
-    launch_ms = timed_ms / max(timed_launches, 1)
-    busy_s = timed_ms / 1e3 if batched else iso_ms * view_launches / 1e3
+    unit's: achieved = gather wave-instructions per second, peak = the rate
+    at which the TD would be 100 % busy at the measured TD cycles per
+    instruction (256 CUs x clock / cycles per instruction), frac = TD busy
+    fraction. The HBM roofline is reported beside it from the memory-side
+    counter bytes. Durations: the un-overlapped HIP-event time of one launch
+    (iso_ms, one stream); rocprofv3's profiled duration is in `pmc`."""
     out = {
         "bound": "td-gather",
         "kernel": "k_sweep (CheckerboardPropagation)",
-        "launch_ms": round(launch_ms, 3),
-        "views_per_launch": streams if batched else 1,
-        "launch_ms_note": ("HIP events on the one launching stream over the timed region; each launch sweeps "
-                           f"{streams} views" if batched else
-                           f"views overlap on {streams} streams: per-view launch time from one view alone"),
-        "launch_ms_single_view": round(iso_ms, 3),
-        "logical_gather_GBs": round(logical_bytes * view_launches / busy_s / 1e9, 1),
+        "launch_ms": round(iso_ms, 3),
+        "launch_ms_note": "HIP events on the engine stream, one launch alone (one photometric + one geometric "
+                          "view on one stream after the timed region); in the timed region "
+                          f"{streams} views share the GPU and a launch spans "
+                          f"{timed_ms / max(timed_launches, 1):.3f} ms",
+        "logical_gather_GBs": round(logical_bytes / (iso_ms / 1e3) / 1e9, 1),
         "logical_note": "SURVEY §8d / BASELINE.md §3 model (36 samples x 5 texels x 4 B per NCC, counted as if "
-                        "uncached) / k_sweep time: a data-volume figure, not an HBM fraction",
+                        "uncached) per launch / launch_ms: a data-volume figure, not an HBM fraction",
     }
     if not pmc or "error" in pmc:
         out.update({"achieved": None, "peak": None, "unit": "Ginst/s", "frac": None, "traffic": None,
                     "pmc": (pmc or {}).get("error", "counter passes skipped")})
         return out
     clock_hz = pmc["clock_ghz"] * 1e9
-    achieved = pmc["gather_insts"] * view_launches / busy_s / 1e9
+    insts = pmc["gather_insts"]
+    achieved = insts / (iso_ms / 1e3) / 1e9
     peak = 256 * clock_hz / pmc["td_cyc_per_inst"] / 1e9
-    hbm_gbs = pmc["hbm_bytes"] * view_launches / busy_s / 1e9
+    hbm_gbs = pmc["hbm_bytes"] / (iso_ms / 1e3) / 1e9
     out.update({
         "achieved": round(achieved, 2),
         "peak": round(peak, 2),
         "unit": "Ginst/s",
-        "frac": round(achieved / peak, 4),
-        "traffic": round(pmc["hbm_bytes"] * out["views_per_launch"]),
-        "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per view-launch x view-launches / k_sweep time; "
-                 "peak = 256 CUs x clock (GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / "
-                 "TA_BUFFER_READ_WAVEFRONTS_sum); pmc.td_busy_frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8) "
-                 "of one-view launches",
+        "frac": round(pmc["td_busy_frac"], 4),
+        "traffic": round(pmc["hbm_bytes"]),
+        "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per launch / launch_ms; peak = 256 CUs x clock "
+                 "(GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / TA_BUFFER_READ_WAVEFRONTS_sum); "
+                 "frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8)",
         "hbm": {
             "bound": "hbm",
             "achieved": round(hbm_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
-            "traffic": round(pmc["hbm_bytes"] * out["views_per_launch"]),
-            "note": "traffic per launch = views_per_launch x (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 of a "
-                    "one-view launch, memory side of L2 (Infinity-Cache hits included), FETCH doubled per the "
-                    "gfx950 calibration",
+            "traffic": round(pmc["hbm_bytes"]),
+            "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 "
+                    "(Infinity-Cache hits included), FETCH doubled per the gfx950 calibration",
         },
         "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
     })

@@ -86,7 +86,6 @@ typedef struct acmmp_timing {
     int32_t sweep_launches; /* 2 * max_iterations */
     float finalize_ms;      /* GetDepthandNormal + Black/Red filter */
     float total_ms;         /* whole RunPatchMatch, device side */
-    int32_t batch_size;     /* engines served by the timed launches (acmmp_run_patchmatch_batch) */
 } acmmp_timing;
 
 /* == struct Problem (src/acmmp_definitions.h:57-63), fixed-size source list. */
@@ -239,16 +238,6 @@ int acmmp_run_patchmatch(acmmp_ctx *ctx);
 /* Asynchronous variant: enqueues the same work on the engine's stream and
  * returns without synchronising (for multi-view pipelining / benchmarks). */
 int acmmp_run_patchmatch_async(acmmp_ctx *ctx);
-/* RunPatchMatch of n engines (n reference views) at once: engines of one
- * device with the same source-view bucket, texel form and max_iterations
- * share every launch (init, each checkerboard sweep, finalize, filter) on
- * the first such engine's stream, up to 4 per launch; the others are grouped
- * alike. Asynchronous: each engine's stream is ordered after its batch, so
- * acmmp_export_results / acmmp_synchronize on any engine see its results.
- * Per engine the results equal acmmp_run_patchmatch's (the reference runs
- * the views one after another, src/main_ACMMP.cpp:123-137). Timing
- * (acmmp_get_timing) is reported by the engine that led the batch. */
-int acmmp_run_patchmatch_batch(acmmp_ctx *const *ctxs, int n);
 /* Waits for all work enqueued on the engine's stream. */
 int acmmp_synchronize(acmmp_ctx *ctx);
 

@@ -31,7 +31,7 @@ def test_every_header_symbol_is_exported(lib):
 def test_struct_layouts():
     assert C.sizeof(_abi.Camera) == 100  # == struct Camera of the reference
     assert C.sizeof(_abi.Params) == 4 * 29
-    assert C.sizeof(_abi.Timing) == 24
+    assert C.sizeof(_abi.Timing) == 20
 
 
 def test_default_params_match_reference(lib):
