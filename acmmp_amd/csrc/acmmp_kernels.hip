@@ -332,13 +332,25 @@ DEV SrcImage src_image(const KViews &kv, int v) {
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------- ref-image tile
-// A block covers 64 colour-split columns (k0..k0+63) x 4 rows (y0..y0+3) of
-// ONE colour c. Both patch offsets i, j are odd, so every reference sample of
-// a colour-c pixel is itself a colour-c pixel: the block's whole reference
-// footprint is a 70 x 14 window of the colour-c plane, staged once in LDS
-// (clamp-to-edge baked in). A wave reads 64 consecutive floats per sample:
-// conflict-free, and the address is a compile-time offset from one base.
-constexpr int kBX = 64, kBY = 4;
+// A block covers kBX colour-split columns (k0..k0+kBX-1) x kBY rows of ONE
+// colour c (256 threads). Both patch offsets i, j are odd, so every
+// reference sample of a colour-c pixel is itself a colour-c pixel: the
+// block's whole reference footprint is a (kBX + 6) x (kBY + 10) window of the
+// colour-c plane, staged once in LDS (clamp-to-edge baked in); the address
+// of a sample is a compile-time offset from the lane's base.
+//
+// ACMMP_BLOCK_X = kBX: 16 (x 16 rows, the default) stacks a block's four
+// 16 x 4 waves vertically, so they share most source-view rows of their
+// patches in the CU's L1, and keeps the ragged last block column narrow
+// (Wh = 800 at 1600 px: 50 x 75 blocks; 64 x 4 blocks gave 12.5 columns).
+// cfg2, ms per k_sweep launch: 64 x 4 4.66, 32 x 8 4.41, 16 x 16 4.28.
+#ifndef ACMMP_BLOCK_X
+#define ACMMP_BLOCK_X 16
+#endif
+constexpr int kBX = ACMMP_BLOCK_X, kBY = 256 / ACMMP_BLOCK_X;
+static_assert(kBX * kBY == 256 && (kBX == 64 || kBX == 32 || kBX == 16), "256-thread blocks");
+// (A tile pitch of 16 mod 32 floats, which puts the two 16-lane rows of a
+// ds_read2_b32 lane group on disjoint banks, measured 0.3 % faster: not kept.)
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
 
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
@@ -919,10 +931,11 @@ DEV BlockXY xcd_block() {
 DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     LaneGeom g;
 #if ACMMP_WAVE2D > 1
-    static_assert(kBX == 64 && kBY == 4 && (ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4), "2D wave map of 64x4 blocks");
-    constexpr int R = ACMMP_WAVE2D, C = 64 / R;
+    // waves of C columns x R rows, kBX / C of them side by side per block row
+    constexpr int R = ACMMP_WAVE2D, C = 64 / R, WPR = kBX / C;
+    static_assert((ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4) && kBX % C == 0 && kBY % R == 0, "2D wave map");
     const int w = tid >> 6, l = tid & 63;
-    const int tx = (w % R) * C + (l % C), ty = (w / R) * R + l / C;
+    const int tx = (w % WPR) * C + (l % C), ty = (w / WPR) * R + l / C;
 #else
     const int tx = tid % kBX, ty = tid / kBX;
 #endif
@@ -1059,16 +1072,16 @@ DEV void wave_sync() {
 // evaluates another lane's item with that lane's pixel, LDS patch weights,
 // tile offset and plane, and returns the cost through LDS. The view stays
 // wave-uniform (scalar SRD and cameras). Result: cmp_res(t, lane) = sum_t.
-template <int TX>
+template <int TX, typename RD, typename RN>
 DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, float4 *lds, const PixPatch &pp,
-                              const ViewCounts &vw, int nsrc, int colour, BlockXY blk, const float *ref_depths,
-                              const float4 *ref_normals, int px, int py) {
+                              const ViewCounts &vw, int nsrc, int colour, BlockXY blk, RD ref_depth,
+                              RN ref_normal, int px, int py) {
     const acmmp_camera &c0 = kv.cam[0];
     const int tid = pp.wo;
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
-        float4 h = ref_normals[t];
-        h.w = distance_to_origin(c0, px, py, ref_depths[t], h);
+        float4 h = ref_normal(t);
+        h.w = distance_to_origin(c0, px, py, ref_depth(t), h);
         lds[t * kThreads + tid] = h;
     }
     cmp_pd(lds, 1, tid) = pp.mean;
@@ -1469,8 +1482,18 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     if (prm.planar_prior) prior_plane = st.prior[center];
     float cost_now = 0.0f, depth_now = 0.0f, restricted_cost = 0.0f, depth_prior = 0.0f;
     float4 plane_now = my_plane;
-    float ref_depths[5];
-    float4 ref_normals[5];
+    // the 5 refinement hypotheses (:735-740) take their depths and normals
+    // from 3 values each: (depth, normal) of t = 1..5 is
+    // (rnd, now), (gen, rnd), (rnd, rnd), (gen, pert), (pert, now), with
+    // gen / now the depth / plane at generation time (held apart: the
+    // accepts below move depth_now and plane_now). Picked by wave-uniform
+    // selects (a dynamically indexed array would live in scratch).
+    float rd_rnd = 0.0f, rd_gen = 0.0f, rd_pert = 0.0f;
+    float4 rn_now = my_plane, rn_rnd = my_plane, rn_pert = my_plane;
+    auto ref_depth = [&](int k) -> float { return k == 4 ? rd_pert : ((k & 1) ? rd_gen : rd_rnd); };
+    auto ref_normal = [&](int k) -> float4 {
+        return (k == 0 || k == 4) ? rn_now : (k == 3 ? rn_pert : rn_rnd);
+    };
     const float gamma = 0.5f;
     const float depth_sigma = (prm.depth_max - prm.depth_min) / 64.0f;
     const float two_dss = 2 * depth_sigma * depth_sigma;
@@ -1478,21 +1501,28 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     const float beta = 0.18f;
 
     for (int t = 0; t < 6; ++t) {
+#if ACMMP_COMPACT_REFINE
+        // all 5 refinement costs at once (their planes go to LDS slots 0..4)
+        if (t == 1)
+            refine_costs_compact<TX>(kv, tile, wlds, cand_lds, pp, vw, nsrc, colour, blk, ref_depth, ref_normal,
+                                     px, py);
+#endif
         float4 h;
         if (t == 0) {
             h = my_plane;
         } else {
-            h = ref_normals[t - 1];
-            h.w = distance_to_origin(c0, px, py, ref_depths[t - 1], h);
+#if ACMMP_COMPACT_REFINE
+            h = cand_lds[(t - 1) * kThreads + pp.wo];  // stored by refine_costs_compact
+#else
+            h = ref_normal(t - 1);
+            h.w = distance_to_origin(c0, px, py, ref_depth(t - 1), h);
+#endif
         }
         // views with a zero sampled weight contribute +0 in the reference
         // (weight 0 * finite cost), so their NCC is skipped: bit-identical
         float tc = 0.0f;
 #if ACMMP_COMPACT_REFINE
         if (t >= 1) {
-            if (t == 1)
-                refine_costs_compact<TX>(kv, tile, wlds, cand_lds, pp, vw, nsrc, colour, blk, ref_depths,
-                                         ref_normals, px, py);
             tc = cmp_res(cand_lds, t - 1, pp.wo);
         } else
 #endif
@@ -1588,15 +1618,16 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
                 depth_perturbed = dm_rng_uniform(&rs) * (dmax_p - dmin_p) + dmin_p;
             } while (depth_perturbed < prm.depth_min && depth_perturbed > prm.depth_max);
             const float4 plane_perturbed = perturbed_normal(c0, px, py, plane_now, rs, kv.pert_pi);
-            ref_depths[0] = depth_rand; ref_normals[0] = plane_now;
-            ref_depths[1] = depth_now;  ref_normals[1] = plane_rand;
-            ref_depths[2] = depth_rand; ref_normals[2] = plane_rand;
-            ref_depths[3] = depth_now;  ref_normals[3] = plane_perturbed;
-            ref_depths[4] = depth_perturbed; ref_normals[4] = plane_now;
+            rd_rnd = depth_rand;
+            rd_gen = depth_now;
+            rd_pert = depth_perturbed;
+            rn_now = plane_now;
+            rn_rnd = plane_rand;
+            rn_pert = plane_perturbed;
         } else {
             const float depth_before = plane_depth(c0, h, px, py);
             if (has_prior) {
-                const float dd = ref_depths[t - 1] - depth_prior;
+                const float dd = ref_depth(t - 1) - depth_prior;
                 const float ad = dm_acosf(dot3(prior_plane, h));
                 const float prior = gamma + dm_expf(-dd * dd / two_dss) * dm_expf(-ad * ad / two_ass);
                 const float rtc = dm_expf(-tc * tc / beta) * prior;

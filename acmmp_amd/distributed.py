@@ -21,6 +21,9 @@ Outputs are the reference's .dmb files, written by the owning rank.
 from __future__ import annotations
 
 import os
+import time
+from collections import defaultdict
+from contextlib import contextmanager
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -151,14 +154,23 @@ def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
         eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
     if t.hierarchy:
         eng.set_hierarchy_inputs(*t.hier_inputs)
+    gpu_ms = 0.0
     eng.run_async()
     if t.planar:
         eng.synchronize()
+        gpu_ms += _run_ms(eng)
         eng.prepare_planar_prior()
         eng.run_async()
     eng.export_results(planes.data_ptr(), costs.data_ptr(), 0)
     eng.synchronize()
-    return ViewResult(planes, costs)
+    gpu_ms += _run_ms(eng)
+    return ViewResult(planes, costs, {"gpu_ms": gpu_ms})
+
+
+def _run_ms(eng: ACMMP) -> float:
+    """Device time (HIP events) of the engine's last RunPatchMatch, 0 when
+    its timing is off."""
+    return eng.timing()["total_ms"] if getattr(eng, "timing_on", False) else 0.0
 
 
 def gpu_jbu(device: int):
@@ -182,7 +194,7 @@ class ViewParallelPipeline:
                  max_iterations: int = 0, geom_iterations: int = 2, group=None,
                  compute: Optional[Callable] = None, jbu: Optional[Callable] = None, write_outputs: bool = True,
                  comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None,
-                 concurrent_views: int = 2):
+                 concurrent_views: int = 2, timing: bool = False):
         self.dense = dense_folder
         self.output_folder = dense_folder + output_dir
         self.device = device
@@ -200,14 +212,21 @@ class ViewParallelPipeline:
         # call), so one view's launches fill the tail of another's
         self.concurrent_views = max(int(concurrent_views), 1)
         self.pool = None
+        # per-phase wall seconds (and summed RunPatchMatch device ms with
+        # timing=True: HIP events around each run, engines' timing on)
+        self.timing = timing
+        self.phase_s = defaultdict(float)
+        self.gpu_ms = 0.0
         self._writer = None  # .dmb writer pool (created on the first write)
         self._pending = []
         if tensor_device is None:
             tensor_device = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
         self.tdev = tensor_device
         if comm_device is None:
-            backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
-            comm_device = self.tdev if backend == "nccl" else torch.device("cpu")
+            # RCCL exchanges device tensors; gloo stages them through the host;
+            # without a process group there is no exchange and the maps stay put
+            backend = dist.get_backend(group) if dist.is_initialized() else None
+            comm_device = torch.device("cpu") if backend == "gloo" else self.tdev
         self.cdev = comm_device
         self.problems = pipeline.generate_sample_list(dense_folder)
         self.index_of = {p.ref_image_id: i for i, p in enumerate(self.problems)}
@@ -267,6 +286,14 @@ class ViewParallelPipeline:
             self.cams[i] = cam
         self._sync()
 
+    @contextmanager
+    def _timed(self, name: str):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.phase_s[name] += time.perf_counter() - t0
+
     def _sync(self):
         """Torch's queued work on the tensor device is complete (the engines'
         streams do not wait on torch's stream)."""
@@ -290,7 +317,9 @@ class ViewParallelPipeline:
             return [self.compute(t, None) for t in tasks]
         if self.pool is None:
             from .resident import EnginePool
-            self.pool = EnginePool(self.device, self.concurrent_views)
+            self.pool = EnginePool(self.device, self.concurrent_views, timing=self.timing)
+            for e in self.pool.engines:
+                e.timing_on = self.timing
         return self.pool.map(lambda eng, t: self.compute(t, eng), tasks)
 
     def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
@@ -307,6 +336,7 @@ class ViewParallelPipeline:
                 prev = self.state[v]
                 t.state = (prev.planes, prev.costs)
             if hierarchy:
+                t_h = time.perf_counter()
                 prev = self.state[v]
                 H, W = t.images[0].shape
                 up = prev.extra["jbu_depth"]
@@ -316,17 +346,21 @@ class ViewParallelPipeline:
                 w = pc if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
                 scaled = np.concatenate([prev.planes[..., :3].cpu().numpy(), w[..., None]], -1).astype(np.float32)
                 t.hier_inputs = (scaled, up)
+                self.phase_s["hier_inputs"] += time.perf_counter() - t_h
             tasks.append(t)
-        self._sync()
-        results = self._map(tasks)
+        with self._timed("compute"):
+            self._sync()
+            results = self._map(tasks)
         local = {}
         for t, res in zip(tasks, results):  # in view order, as the sequential loop
             v = t.index
             self.state[v] = res
+            self.gpu_ms += res.extra.get("gpu_ms", 0.0)
             local[v] = res.planes[..., 3]
             if self.write_outputs:
                 self._write(t.ref_id, res, geom)
-        self.depths = exchange.gather(self.rank, local)
+        with self._timed("exchange"):
+            self.depths = exchange.gather(self.rank, local)
         self.pass_index += 1
 
     def _write(self, ref_id: int, res: ViewResult, geom: bool):
@@ -378,25 +412,28 @@ class ViewParallelPipeline:
         try:
             while max_down >= 0:
                 pipeline.scale_step(self.problems)
-                self._load_views()
+                with self._timed("load"):
+                    self._load_views()
                 exchange = DepthExchange(self.assignment, self._shapes(), self.cdev, self.group,
                                          out_device=self.tdev)
                 if first:
                     first = False
                     self.run_pass(False, True, False, False, exchange)
                 else:
-                    for v in self.mine:  # JointBilateralUpsampling, in memory
-                        p = self.problems[v]
-                        img = self.images[p.ref_image_id].cpu().numpy()
-                        up, isc = self.jbu(img, self.state[v].planes[..., 3].cpu().numpy())
-                        if up is None:
-                            raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
-                        self.state[v].extra["jbu_depth"] = up
+                    with self._timed("jbu"):
+                        for v in self.mine:  # JointBilateralUpsampling, in memory
+                            p = self.problems[v]
+                            img = self.images[p.ref_image_id].cpu().numpy()
+                            up, isc = self.jbu(img, self.state[v].planes[..., 3].cpu().numpy())
+                            if up is None:
+                                raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
+                            self.state[v].extra["jbu_depth"] = up
                     self.run_pass(False, True, True, False, exchange)
                 for g in range(self.geom_iterations):
                     self.run_pass(True, False, False, g > 0, exchange)
                 max_down -= 1
-            self._flush_writes()
+            with self._timed("flush_writes"):
+                self._flush_writes()
         except BaseException:
             try:
                 self._flush_writes()  # no write is left running; the pass's error wins

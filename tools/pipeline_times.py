@@ -15,7 +15,8 @@ same folder runs on one GPU through
 Synthetic, seeded scene rendered on the GPU and written as 8-bit JPEGs (a
 COLMAP-converted dense folder); wall times include JPEG decode and .dmb I/O,
 as the reference's do. Iterations: the driver's default (the reference's).
-usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] > gpurun_out/pipeline.jsonl
+usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] [steps] > gpurun_out/pipeline.jsonl
+  steps: comma list of distributed,cli,fusion (default all; fusion needs cli)
 """
 import json
 import os
@@ -38,6 +39,7 @@ V = int(sys.argv[1]) if len(sys.argv) > 1 else 49
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 1600
 H = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
 NSRC = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+STEPS = set((sys.argv[5] if len(sys.argv) > 5 else "distributed,cli,fusion").split(","))
 
 
 def emit(**kw):
@@ -60,11 +62,21 @@ def main():
     scene.write_dense_folder(sc, dense, num_src=NSRC)
     emit(step="write_dense", views=V, width=W, height=H, nsrc=NSRC, s=round(time.perf_counter() - t0, 2))
 
-    t0 = time.perf_counter()
-    ViewParallelPipeline(dense, "/ACMMP_dist", device=0, concurrent_views=2).run()
-    torch.cuda.synchronize()
-    emit(step="distributed_world1", order="jacobi", concurrent_views=2, s=round(time.perf_counter() - t0, 2))
-    shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
+    if "distributed" in STEPS:
+        t0 = time.perf_counter()
+        pipe = ViewParallelPipeline(dense, "/ACMMP_dist", device=0, concurrent_views=2, timing=True)
+        pipe.run()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        # gpu_runpatchmatch_s: the runs' HIP-event durations summed (two views
+        # overlap on the GPU, so the sum can exceed the compute phase's wall)
+        emit(step="distributed_world1", order="jacobi", concurrent_views=2, s=round(wall, 2),
+             gpu_runpatchmatch_s=round(pipe.gpu_ms / 1e3, 2),
+             phases_s={k: round(v, 2) for k, v in sorted(pipe.phase_s.items())})
+        shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
+    if "cli" not in STEPS:
+        shutil.rmtree(tmp, ignore_errors=True)
+        return
 
     cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
     t0 = time.perf_counter()

@@ -11,7 +11,7 @@ for spec in "$@"; do
   i=0
   for set in "$P1" "$P2"; do
     i=$((i+1))
-    ACMMP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc $set -f csv -d gpurun_out/ab_$name/p$i -o run -- \
+    ACMMP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --kernel-include-regex k_sweep --pmc $set -f csv -d gpurun_out/ab_$name/p$i -o run -- \
       python3 tools/quick_time.py 1600 1200 8 > gpurun_out/ab_${name}_p$i.log 2>&1
     rc=$?
     echo "$name pass $i rc=$rc"
