@@ -162,6 +162,7 @@ SIGNATURES = {
     "acmmp_export_results": (C.c_int, [_CTX, C.c_void_p, C.c_void_p, C.c_void_p]),
     "acmmp_set_plane_hypotheses": (C.c_int, [_CTX, _FP, _FP]),
     "acmmp_set_hierarchy_inputs": (C.c_int, [_CTX, _FP, C.c_int, C.c_int, _FP]),
+    "acmmp_set_hierarchy_inputs_device": (C.c_int, [_CTX, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "acmmp_set_seed_prior": (C.c_int, [_CTX, _FP]),
     "acmmp_set_planar_prior": (C.c_int, [_CTX, _FP, C.c_int, _U32P]),
     "acmmp_get_support_points": (C.c_int, [_CTX, _I32P, C.c_int, C.POINTER(C.c_int)]),
@@ -171,6 +172,8 @@ SIGNATURES = {
     "acmmp_prepare_planar_prior": (C.c_int, [_CTX, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "acmmp_joint_bilateral_upsample": (C.c_int, [C.c_int, _FP, C.c_int, C.c_int, _FP, C.c_int, C.c_int, _FP,
                                                  C.POINTER(C.c_int)]),
+    "acmmp_joint_bilateral_upsample_device": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                                        C.c_int, C.c_void_p, C.POINTER(C.c_int)]),
     "acmmp_run_patchmatch": (C.c_int, [_CTX]),
     "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
     "acmmp_synchronize": (C.c_int, [_CTX]),

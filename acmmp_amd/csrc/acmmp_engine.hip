@@ -526,21 +526,31 @@ int acmmp_export_results(acmmp_ctx *ctx, float *d_planes4, float *d_costs, float
     return ACMMP_OK;
 }
 
-int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w, int scaled_h,
-                               const float *upsampled_depth) {
+namespace {
+int set_hierarchy_impl(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w, int scaled_h,
+                       const float *upsampled_depth, bool device_src) {
     int rc = check_ready(ctx);
     if (rc) return rc;
     if (!scaled_planes4 || !upsampled_depth || scaled_w <= 0 || scaled_h <= 0)
         return set_err(ctx, ACMMP_ERR_ARG, "bad hierarchy inputs");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
     const size_t S = (size_t)scaled_w * scaled_h;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still read the old inputs
     HIP_TRY(ctx, dalloc(ctx->d_scaled, S));
     ctx->scaled_count = S;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_scaled, scaled_planes4, S * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_scaled, scaled_planes4, S * sizeof(float4),
+                                device_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
     // plane_hypotheses_host[center].w = ref_depth; x, y, z never written (pinned 0)
     const size_t P = (size_t)ctx->W * ctx->H;
-    std::vector<float> tmp(P * 4, 0.0f);
-    for (size_t i = 0; i < P; ++i) tmp[i * 4 + 3] = upsampled_depth[i];
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, tmp.data(), P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    if (device_src) {
+        HIP_TRY(ctx, launch_depth_planes(upsampled_depth, P, ctx->d_rm_plane, ctx->stream));
+    } else {
+        std::vector<float> tmp(P * 4, 0.0f);
+        for (size_t i = 0; i < P; ++i) tmp[i * 4 + 3] = upsampled_depth[i];
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, tmp.data(), P * sizeof(float4), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // tmp goes out of scope
+    }
     // `if (width != images[0].rows || height != images[0].cols)` (src/ACMMP.cpp:766), swap included
     if (scaled_w != ctx->H || scaled_h != ctx->W) {
         ctx->prm.upsample = 1;
@@ -549,9 +559,19 @@ int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int 
     } else {
         ctx->prm.upsample = 0;
     }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->have_scaled = true;
     return ACMMP_OK;
+}
+}  // namespace
+
+int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w, int scaled_h,
+                               const float *upsampled_depth) {
+    return set_hierarchy_impl(ctx, scaled_planes4, scaled_w, scaled_h, upsampled_depth, false);
+}
+
+int acmmp_set_hierarchy_inputs_device(acmmp_ctx *ctx, const float *d_scaled_planes4, int scaled_w, int scaled_h,
+                                      const float *d_upsampled_depth) {
+    return set_hierarchy_impl(ctx, d_scaled_planes4, scaled_w, scaled_h, d_upsampled_depth, true);
 }
 
 int acmmp_set_seed_prior(acmmp_ctx *ctx, const float *planes4) {
@@ -799,6 +819,24 @@ int acmmp_joint_bilateral_upsample(int device, const float *image, int width, in
     if (d_img) (void)hipFree(d_img);
     if (d_dep) (void)hipFree(d_dep);
     if (d_out) (void)hipFree(d_out);
+    if (s) (void)hipStreamDestroy(s);
+    return e == hipSuccess ? ACMMP_OK : ACMMP_ERR_HIP;
+}
+
+int acmmp_joint_bilateral_upsample_device(int device, const float *d_image, int width, int height,
+                                          const float *d_depth, int depth_width, int depth_height, float *d_out,
+                                          int *image_scale) {
+    if (!d_image || !d_depth || !d_out || width <= 0 || height <= 0 || depth_width <= 0 || depth_height <= 0)
+        return ACMMP_ERR_ARG;
+    const int isc = std::max(height / depth_height, width / depth_width);  // RunJBU (src/ACMMP.cpp:1012-1021)
+    if (image_scale) *image_scale = isc;
+    if (isc <= 1) return ACMMP_OK;
+    if (isc > 64) return ACMMP_ERR_UNSUPPORTED;
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = launch_jbu(d_image, width, height, d_depth, depth_width, depth_height, isc, d_out, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (s) (void)hipStreamDestroy(s);
     return e == hipSuccess ? ACMMP_OK : ACMMP_ERR_HIP;
 }

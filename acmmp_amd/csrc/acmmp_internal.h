@@ -105,6 +105,7 @@ hipError_t launch_pad_h16(const float *src, int spitch, int W, int H, void *dst,
 hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch,
                            uint32_t *not_u8, hipStream_t stream);
 int diag_read_cycles(unsigned long long *out8);
+hipError_t launch_depth_planes(const float *depth, size_t n, float4 *out, hipStream_t stream);
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);

@@ -35,12 +35,13 @@ constexpr int kTaps = 6;
 
 // Build options of the gather kernels (each an A/B-measured choice; the
 // defaults are the measured winners):
+//   ACMMP_BLOCK_X        colour-split columns per block (x 256/X rows)
 //   ACMMP_WAVE2D         rows of pixels per wave (lane_geom_of)
 //   ACMMP_CAND_LDS       the 8 candidate planes staged in LDS (k_sweep)
 //   ACMMP_COMPACT_REFINE refinement items packed across lanes (refine_costs_compact)
 //   ACMMP_PIPE_ROWS      software-pipelined patch rows (ncc_sums_rows)
 #ifndef ACMMP_WAVE2D
-#define ACMMP_WAVE2D 4
+#define ACMMP_WAVE2D 8
 #endif
 #ifndef ACMMP_CAND_LDS
 #define ACMMP_CAND_LDS 1
@@ -339,16 +340,18 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // colour-c plane, staged once in LDS (clamp-to-edge baked in); the address
 // of a sample is a compile-time offset from the lane's base.
 //
-// ACMMP_BLOCK_X = kBX: 16 (x 16 rows, the default) stacks a block's four
-// 16 x 4 waves vertically, so they share most source-view rows of their
-// patches in the CU's L1, and keeps the ragged last block column narrow
-// (Wh = 800 at 1600 px: 50 x 75 blocks; 64 x 4 blocks gave 12.5 columns).
-// cfg2, ms per k_sweep launch: 64 x 4 4.66, 32 x 8 4.41, 16 x 16 4.28.
+// ACMMP_BLOCK_X = kBX: 16 (x 16 rows, the default) packs a block's four
+// waves (8 x 8 colour-split pixels each, ACMMP_WAVE2D) 2 x 2, so they share
+// most source-view rows of their patches in the CU's L1, and keeps the
+// ragged last block column narrow (Wh = 800 at 1600 px: 50 x 75 blocks;
+// 64 x 4 blocks gave 12.5 columns). cfg2, ms per k_sweep launch
+// (profiles/r02_block_shape.md): 64 x 4 blocks of 16 x 4 waves 4.66,
+// 32 x 8 4.41, 16 x 16 4.28, 16 x 16 of 8 x 8 waves 4.19, 8 x 32 4.18.
 #ifndef ACMMP_BLOCK_X
 #define ACMMP_BLOCK_X 16
 #endif
 constexpr int kBX = ACMMP_BLOCK_X, kBY = 256 / ACMMP_BLOCK_X;
-static_assert(kBX * kBY == 256 && (kBX == 64 || kBX == 32 || kBX == 16), "256-thread blocks");
+static_assert(kBX * kBY == 256 && (kBX == 64 || kBX == 32 || kBX == 16 || kBX == 8), "256-thread blocks");
 // (A tile pitch of 16 mod 32 floats, which puts the two 16-lane rows of a
 // ds_read2_b32 lane group on disjoint banks, measured 0.3 % faster: not kept.)
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
@@ -924,7 +927,7 @@ DEV BlockXY xcd_block() {
     return b;
 }
 
-// ACMMP_WAVE2D = R rows per wave (1, 2 or 4): each wave covers 64/R columns
+// ACMMP_WAVE2D = R rows per wave (1, 2, 4 or 8): each wave covers 64/R columns
 // x R rows of the block instead of one 64-column row, so its gathers for
 // neighbouring patch rows overlap in the source image (L1 reuse within a
 // wave); the lane -> pixel map is all that changes.
@@ -933,7 +936,8 @@ DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
 #if ACMMP_WAVE2D > 1
     // waves of C columns x R rows, kBX / C of them side by side per block row
     constexpr int R = ACMMP_WAVE2D, C = 64 / R, WPR = kBX / C;
-    static_assert((ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4) && kBX % C == 0 && kBY % R == 0, "2D wave map");
+    static_assert((ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4 || ACMMP_WAVE2D == 8) && kBX % C == 0 && kBY % R == 0,
+                  "2D wave map");
     const int w = tid >> 6, l = tid & 63;
     const int tx = (w % WPR) * C + (l % C), ty = (w / WPR) * R + l / C;
 #else
@@ -1933,6 +1937,20 @@ __global__ __launch_bounds__(256) void k_jbu(const float *__restrict__ img, int 
 }
 
 // ---------------------------------------------------------------- launchers
+// plane_hypotheses_host[center] = (0, 0, 0, depth) for the hierarchy init
+// (src/ACMMP.cpp:797-804: x, y, z never written, pinned 0)
+__global__ __launch_bounds__(256) void k_depth_planes(const float *__restrict__ depth, size_t n,
+                                                      float4 *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = make_float4(0.0f, 0.0f, 0.0f, depth[i]);
+}
+
+hipError_t launch_depth_planes(const float *depth, size_t n, float4 *out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    k_depth_planes<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream>>>(depth, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream) {
     dim3 block(64, 4), grid((W + 63) / 64, (H + 3) / 4);

@@ -34,7 +34,7 @@ import torch.distributed as dist
 from . import _abi
 from . import io as aio
 from . import pipeline
-from .engine import ACMMP, AcmmpError, joint_bilateral_upsample
+from .engine import ACMMP, AcmmpError, joint_bilateral_upsample_device
 
 
 def lpt_assign(costs: list, world: int) -> list:
@@ -109,7 +109,7 @@ class ViewTask:
     max_iterations: int
     depths: Optional[list] = None          # source depth maps (tensor views, any row pitch), geom passes
     state: Optional[tuple] = None          # (planes (H,W,4), costs (H,W)) tensors, geom passes
-    hier_inputs: Optional[tuple] = None    # (scaled planes (sh,sw,4), upsampled depth (H,W)) numpy
+    hier_inputs: Optional[tuple] = None    # (scaled planes (sh,sw,4), upsampled depth (H,W)) tensors
 
 
 @dataclass
@@ -153,7 +153,8 @@ def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
         eng.set_depth_maps_device([d.data_ptr() for d in t.depths], [d.stride(0) for d in t.depths])
         eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
     if t.hierarchy:
-        eng.set_hierarchy_inputs(*t.hier_inputs)
+        scaled, up = t.hier_inputs
+        eng.set_hierarchy_inputs_device(scaled.data_ptr(), scaled.shape[1], scaled.shape[0], up.data_ptr())
     gpu_ms = 0.0
     eng.run_async()
     if t.planar:
@@ -174,8 +175,16 @@ def _run_ms(eng: ACMMP) -> float:
 
 
 def gpu_jbu(device: int):
-    def run(image: np.ndarray, depth: np.ndarray):
-        return joint_bilateral_upsample(image, depth, device)
+    """JointBilateralUpsampling on resident tensors: (upsampled depth tensor at
+    the image's size or None, Imagescale)."""
+    def run(image: torch.Tensor, depth: torch.Tensor):
+        image = image.contiguous()
+        depth = depth.contiguous()
+        out = torch.empty_like(image)
+        torch.cuda.current_stream(image.device).synchronize()  # the JBU stream does not wait on torch's
+        isc = joint_bilateral_upsample_device(image.data_ptr(), image.shape[1], image.shape[0], depth.data_ptr(),
+                                              depth.shape[1], depth.shape[0], out.data_ptr(), device)
+        return (out if isc > 1 else None), isc
     return run
 
 
@@ -342,10 +351,9 @@ class ViewParallelPipeline:
                 up = prev.extra["jbu_depth"]
                 sh, sw = prev.costs.shape
                 upsample = sw != H or sh != W  # src/ACMMP.cpp:766, rows/cols swap included
-                pc = prev.costs.cpu().numpy()
-                w = pc if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
-                scaled = np.concatenate([prev.planes[..., :3].cpu().numpy(), w[..., None]], -1).astype(np.float32)
-                t.hier_inputs = (scaled, up)
+                w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
+                scaled = torch.cat([prev.planes[..., :3], w[..., None]], -1).contiguous()
+                t.hier_inputs = (scaled, up.contiguous())
                 self.phase_s["hier_inputs"] += time.perf_counter() - t_h
             tasks.append(t)
         with self._timed("compute"):
@@ -421,10 +429,10 @@ class ViewParallelPipeline:
                     self.run_pass(False, True, False, False, exchange)
                 else:
                     with self._timed("jbu"):
-                        for v in self.mine:  # JointBilateralUpsampling, in memory
+                        for v in self.mine:  # JointBilateralUpsampling, resident
                             p = self.problems[v]
-                            img = self.images[p.ref_image_id].cpu().numpy()
-                            up, isc = self.jbu(img, self.state[v].planes[..., 3].cpu().numpy())
+                            img = self.images[p.ref_image_id]
+                            up, isc = self.jbu(img, self.state[v].planes[..., 3])
                             if up is None:
                                 raise AcmmpError(f"view {p.ref_image_id}: JBU image scale 1 (nothing to upsample)")
                             self.state[v].extra["jbu_depth"] = up

@@ -79,6 +79,21 @@ def joint_bilateral_upsample(image: np.ndarray, depth: np.ndarray, device: int =
     return (None if isc.value <= 1 else out), isc.value
 
 
+def joint_bilateral_upsample_device(d_image: int, width: int, height: int, d_depth: int, depth_width: int,
+                                    depth_height: int, d_out: int, device: int = 0) -> int:
+    """joint_bilateral_upsample on device buffers (row-major, unpadded
+    float32: image and out width x height, depth depth_width x
+    depth_height). Returns Imagescale; d_out is written only when it is > 1."""
+    lib = _abi.load_library()
+    isc = C.c_int(0)
+    rc = lib.acmmp_joint_bilateral_upsample_device(int(device), C.c_void_p(int(d_image)), int(width), int(height),
+                                                   C.c_void_p(int(d_depth)), int(depth_width), int(depth_height),
+                                                   C.c_void_p(int(d_out)), C.byref(isc))
+    if rc != 0:
+        raise AcmmpError(f"acmmp_joint_bilateral_upsample_device failed (status {rc})")
+    return isc.value
+
+
 def device_count() -> int:
     return int(_abi.load_library().acmmp_device_count())
 
@@ -219,6 +234,16 @@ class ACMMP:
         sh, sw = sp.shape[:2]
         self._check(self._lib.acmmp_set_hierarchy_inputs(self._ctx, _fptr(sp), sw, sh, _fptr(ud)),
                     "acmmp_set_hierarchy_inputs")
+
+    def set_hierarchy_inputs_device(self, d_scaled_planes: int, scaled_w: int, scaled_h: int,
+                                    d_upsampled_depth: int):
+        """Hierarchy inputs from device buffers (scaled planes scaled_h x
+        scaled_w float4, upsampled depth at the reference size); they must
+        stay valid until the next run has completed."""
+        self._check(self._lib.acmmp_set_hierarchy_inputs_device(self._ctx, C.c_void_p(int(d_scaled_planes)),
+                                                                int(scaled_w), int(scaled_h),
+                                                                C.c_void_p(int(d_upsampled_depth))),
+                    "acmmp_set_hierarchy_inputs_device")
 
     def SetPlanarPrior(self, prior: np.ndarray):
         """Seeded plane priors (src/ACMMP.cpp:476-523); sets params.seeded."""

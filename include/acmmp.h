@@ -180,6 +180,10 @@ int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, co
  * rows/cols swap. */
 int acmmp_set_hierarchy_inputs(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w,
                                int scaled_h, const float *upsampled_depth);
+/* Same from device buffers (the view-parallel driver keeps them resident):
+ * copied / expanded on the engine stream, ordered before the next run. */
+int acmmp_set_hierarchy_inputs_device(acmmp_ctx *ctx, const float *d_scaled_planes4, int scaled_w,
+                                      int scaled_h, const float *d_upsampled_depth);
 
 /* ~ ACMMP::SetPlanarPrior(unique_ptr<float4>) (src/ACMMP.cpp:476-523): seeded
  * plane priors, float4 per ref pixel (camera-frame normal, distance). Sets
@@ -230,6 +234,12 @@ int acmmp_prepare_planar_prior(acmmp_ctx *ctx, int *num_support_points, int *num
  * computed or written, as in the reference. Host buffers in and out. */
 int acmmp_joint_bilateral_upsample(int device, const float *image, int width, int height, const float *depth,
                                    int depth_width, int depth_height, float *out, int *image_scale);
+/* Same on device buffers (row-major, unpadded): d_image width x height,
+ * d_depth depth_width x depth_height, d_out width x height. Returns when
+ * d_out is written. */
+int acmmp_joint_bilateral_upsample_device(int device, const float *d_image, int width, int height,
+                                          const float *d_depth, int depth_width, int depth_height, float *d_out,
+                                          int *image_scale);
 
 /* ~ ACMMP::RunPatchMatch (src/ACMMP.cu:1378-1456): init, max_iterations x
  * (black, red) checkerboard sweeps, depth/normal conversion, black/red median

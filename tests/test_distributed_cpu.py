@@ -44,7 +44,7 @@ def fake_compute(t, eng=None):
         depth = depth + sum(float(d.cpu().double().mean()) for d in t.depths) / 100.0
         depth = depth + t.state[0][..., 3].cpu().numpy() / 1000.0 + (7.0 if t.multi else 0.0)
     if t.hierarchy:
-        depth = depth + t.hier_inputs[1] / 100.0 + float(t.hier_inputs[0].mean())
+        depth = depth + t.hier_inputs[1].cpu().numpy() / 100.0 + float(t.hier_inputs[0].double().mean())
     planes = np.zeros((H, W, 4), np.float32)
     planes[..., 2] = -1.0
     planes[..., 3] = depth
@@ -55,10 +55,11 @@ def fake_compute(t, eng=None):
 
 
 def fake_jbu(image, depth):
+    """Tensors in, tensor out, like the driver's gpu_jbu."""
     H, W = image.shape
     ys = (np.arange(H) * depth.shape[0] // H)[:, None]
     xs = (np.arange(W) * depth.shape[1] // W)[None, :]
-    return depth[ys, xs].astype(np.float32), 2
+    return torch.from_numpy(depth.cpu().numpy()[ys, xs].astype(np.float32)), 2
 
 
 def _worker(rank, world, port, dense, out_dir, q):

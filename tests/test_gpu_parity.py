@@ -299,8 +299,9 @@ def test_planar_prior_init_branch_with_geom(small_scene):
     assert_bit_exact(got[1], ref["costs"], "costs")
 
 
+@pytest.mark.parametrize("device_inputs", [False, True])
 @pytest.mark.parametrize("same_size", [False, True])
-def test_hierarchy_init(small_scene, same_size):
+def test_hierarchy_init(small_scene, same_size, device_inputs):
     """Hierarchical init (src/ACMMP.cpp:745-808, src/ACMMP.cu:663-703):
     upsample branch (upscale_normal) from a half-resolution map, and the
     non-upsample branch reached through the reference's rows/cols swap
@@ -324,7 +325,14 @@ def test_hierarchy_init(small_scene, same_size):
     with ACMMP(0) as eng:
         eng.set_params(p)
         eng.set_images(cams, imgs)
-        eng.set_hierarchy_inputs(scaled, up_depth)
+        if device_inputs:  # acmmp_set_hierarchy_inputs_device (the view-parallel driver's path)
+            import torch
+            ts = torch.from_numpy(scaled).cuda()
+            tu = torch.from_numpy(up_depth).cuda()
+            torch.cuda.synchronize()
+            eng.set_hierarchy_inputs_device(ts.data_ptr(), sw, sh, tu.data_ptr())
+        else:
+            eng.set_hierarchy_inputs(scaled, up_depth)
         prm = eng.params
         eng.RunPatchMatch()
         got = (eng.plane_hypotheses(), eng.costs())
