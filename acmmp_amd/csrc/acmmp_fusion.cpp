@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/acmmp.h"
+#include "acmmp_hostio.h"
 
 namespace {
 
@@ -270,8 +271,6 @@ void candidates(const FusionInputs &in, const std::vector<std::vector<uint8_t>> 
 
 }  // namespace
 
-// in acmmp_pipeline.cpp (zlib PNG writer)
-int acmmp_internal_write_png_gray(const char *path, int w, int h, const uint8_t *px);
 
 extern "C" {
 
@@ -466,7 +465,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         }
         if (write_debug_images) {
             const std::string dbg = dense + "/approved_pixels_cam_" + std::to_string(i) + ".png";
-            if (acmmp_internal_write_png_gray(dbg.c_str(), W, H, approved.data()))
+            if (acmmp_internal_write_png(dbg.c_str(), W, H, 1, approved.data()))
                 return ffail(ACMMP_ERR_IO, "cannot write %s", dbg.c_str());
         }
     }

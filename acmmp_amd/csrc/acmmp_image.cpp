@@ -23,6 +23,7 @@
 #include <zlib.h>
 
 #include "../../include/acmmp.h"
+#include "acmmp_hostio.h"
 
 namespace {
 
@@ -276,10 +277,13 @@ constexpr int kConstBits = 13, kPass1Bits = 2;
 constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633,
                   F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
 
-inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+// Intermediates are 64-bit like libjpeg-turbo's JLONG on LP64 (the
+// workspace is int), so out-of-range coefficients of a corrupt stream wrap
+// instead of overflowing a signed int.
+inline int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
 
-inline uint8_t range_limit(int32_t x) {
-    const int idx = x & 1023;  // RANGE_MASK of the post-IDCT table (jdmaster.c)
+inline uint8_t range_limit(int64_t x) {
+    const int idx = (int)(x & 1023);  // RANGE_MASK of the post-IDCT table (jdmaster.c)
     if (idx < 128) return (uint8_t)(idx + 128);
     if (idx < 512) return 255;
     if (idx < 896) return 0;
@@ -292,28 +296,28 @@ void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) 
         const int16_t *ip = in + c;
         const uint16_t *qp = q + c;
         if (!ip[8] && !ip[16] && !ip[24] && !ip[32] && !ip[40] && !ip[48] && !ip[56]) {
-            const int32_t dc = ((int32_t)ip[0] * qp[0]) << kPass1Bits;
+            const int32_t dc = (int32_t)((uint32_t)((int32_t)ip[0] * qp[0]) << kPass1Bits);  // LEFT_SHIFT
             for (int r = 0; r < 8; ++r) ws[r * 8 + c] = dc;
             continue;
         }
-        int32_t z2 = (int32_t)ip[16] * qp[16], z3 = (int32_t)ip[48] * qp[48];
-        int32_t z1 = (z2 + z3) * F0541;
-        int32_t tmp2 = z1 + z3 * (-F1847);
-        int32_t tmp3 = z1 + z2 * F0765;
-        z2 = (int32_t)ip[0] * qp[0];
-        z3 = (int32_t)ip[32] * qp[32];
-        int32_t tmp0 = (z2 + z3) * (1 << kConstBits);
-        int32_t tmp1 = (z2 - z3) * (1 << kConstBits);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-        tmp0 = (int32_t)ip[56] * qp[56];
-        tmp1 = (int32_t)ip[40] * qp[40];
-        tmp2 = (int32_t)ip[24] * qp[24];
-        tmp3 = (int32_t)ip[8] * qp[8];
+        int64_t z2 = (int64_t)ip[16] * qp[16], z3 = (int64_t)ip[48] * qp[48];
+        int64_t z1 = (z2 + z3) * F0541;
+        int64_t tmp2 = z1 + z3 * (-F1847);
+        int64_t tmp3 = z1 + z2 * F0765;
+        z2 = (int64_t)ip[0] * qp[0];
+        z3 = (int64_t)ip[32] * qp[32];
+        int64_t tmp0 = (z2 + z3) * ((int64_t)1 << kConstBits);
+        int64_t tmp1 = (z2 - z3) * ((int64_t)1 << kConstBits);
+        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = (int64_t)ip[56] * qp[56];
+        tmp1 = (int64_t)ip[40] * qp[40];
+        tmp2 = (int64_t)ip[24] * qp[24];
+        tmp3 = (int64_t)ip[8] * qp[8];
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F1175;
+        int64_t z4 = tmp1 + tmp3;
+        const int64_t z5 = (z3 + z4) * F1175;
         tmp0 *= F0298;
         tmp1 *= F2053;
         tmp2 *= F3072;
@@ -329,26 +333,26 @@ void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) 
         tmp2 += z2 + z3;
         tmp3 += z1 + z4;
         const int sh = kConstBits - kPass1Bits;
-        ws[0 * 8 + c] = descale(tmp10 + tmp3, sh);
-        ws[7 * 8 + c] = descale(tmp10 - tmp3, sh);
-        ws[1 * 8 + c] = descale(tmp11 + tmp2, sh);
-        ws[6 * 8 + c] = descale(tmp11 - tmp2, sh);
-        ws[2 * 8 + c] = descale(tmp12 + tmp1, sh);
-        ws[5 * 8 + c] = descale(tmp12 - tmp1, sh);
-        ws[3 * 8 + c] = descale(tmp13 + tmp0, sh);
-        ws[4 * 8 + c] = descale(tmp13 - tmp0, sh);
+        ws[0 * 8 + c] = (int32_t)descale(tmp10 + tmp3, sh);
+        ws[7 * 8 + c] = (int32_t)descale(tmp10 - tmp3, sh);
+        ws[1 * 8 + c] = (int32_t)descale(tmp11 + tmp2, sh);
+        ws[6 * 8 + c] = (int32_t)descale(tmp11 - tmp2, sh);
+        ws[2 * 8 + c] = (int32_t)descale(tmp12 + tmp1, sh);
+        ws[5 * 8 + c] = (int32_t)descale(tmp12 - tmp1, sh);
+        ws[3 * 8 + c] = (int32_t)descale(tmp13 + tmp0, sh);
+        ws[4 * 8 + c] = (int32_t)descale(tmp13 - tmp0, sh);
     }
     const int sh = kConstBits + kPass1Bits + 3;
     for (int r = 0; r < 8; ++r) {
         const int32_t *w = ws + r * 8;
         uint8_t *o = out + (size_t)r * stride;
-        int32_t z2 = w[2], z3 = w[6];
-        int32_t z1 = (z2 + z3) * F0541;
-        int32_t tmp2 = z1 + z3 * (-F1847);
-        int32_t tmp3 = z1 + z2 * F0765;
-        int32_t tmp0 = (w[0] + w[4]) * (1 << kConstBits);
-        int32_t tmp1 = (w[0] - w[4]) * (1 << kConstBits);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        int64_t z2 = w[2], z3 = w[6];
+        int64_t z1 = (z2 + z3) * F0541;
+        int64_t tmp2 = z1 + z3 * (-F1847);
+        int64_t tmp3 = z1 + z2 * F0765;
+        int64_t tmp0 = (w[0] + w[4]) * ((int64_t)1 << kConstBits);
+        int64_t tmp1 = (w[0] - w[4]) * ((int64_t)1 << kConstBits);
+        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
         tmp0 = w[7];
         tmp1 = w[5];
         tmp2 = w[3];
@@ -356,8 +360,8 @@ void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) 
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F1175;
+        int64_t z4 = tmp1 + tmp3;
+        const int64_t z5 = (z3 + z4) * F1175;
         tmp0 *= F0298;
         tmp1 *= F2053;
         tmp2 *= F3072;
@@ -515,6 +519,10 @@ int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H,
             const int mcus_y = (j.H + 8 * j.vmax - 1) / (8 * j.vmax);
             y.bw = mcus_x * y.h;
             y.bh = mcus_y * y.v;
+            // a complete scan spends >= 2 bits per block (DC + EOB codes), so
+            // a header claiming more than 8 blocks per file byte is corrupt
+            // (checked before allocating from it)
+            if ((size_t)mcus_x * mcus_y * j.hmax * j.vmax > 8 * buf.size() + 4096) return ACMMP_ERR_IO;
             y.coef.assign((size_t)y.bw * y.bh * 64, 0);
             if (bgr) {
                 if (j.ncomp != 1 && j.ncomp != 3) return ACMMP_ERR_UNSUPPORTED;  // CMYK / YCCK
@@ -632,11 +640,11 @@ int pnm_decode(const std::vector<uint8_t> &b, bool size_only, int &W, int &H, st
     if (size_only) return ACMMP_OK;
     ++o;  // single whitespace after the header
     const size_t P = (size_t)W * H;
-    out->resize(P);
     if (magic == "P5") {
         const int maxv = std::atoi(tm.c_str());
         const int bps = maxv > 255 ? 2 : 1;
         if (maxv <= 0 || maxv > 65535 || o + P * bps > b.size()) return ACMMP_ERR_IO;
+        out->resize(P);
         for (size_t i = 0; i < P; ++i)
             (*out)[i] = bps == 1 ? (float)b[o + i] : (float)((b[o + 2 * i] << 8) | b[o + 2 * i + 1]);
         return ACMMP_OK;
@@ -644,6 +652,7 @@ int pnm_decode(const std::vector<uint8_t> &b, bool size_only, int &W, int &H, st
     if (magic == "Pf") {  // grayscale PFM: rows bottom-to-top, scale sign = endianness
         const double scale = std::atof(tm.c_str());
         if (o + P * 4 > b.size()) return ACMMP_ERR_IO;
+        out->resize(P);
         const bool little = scale < 0;
         for (int r = 0; r < H; ++r)
             for (int c = 0; c < W; ++c) {
@@ -711,6 +720,9 @@ int png_decode(const std::vector<uint8_t> &b, int &W, int &H, int &C, int &depth
     if (C == 0) return ACMMP_ERR_UNSUPPORTED;  // palette
     if (!out) return ACMMP_OK;
     const size_t bpp = (size_t)C * depth / 8, stride = bpp * W;
+    // zlib inflates at most ~1032:1: a header implying more raw bytes than
+    // that is corrupt (checked before allocating from it)
+    if ((stride + 1) * (size_t)H / 1032 > z.size() + 1) return ACMMP_ERR_IO;
     std::vector<uint8_t> raw((stride + 1) * H);
     uLongf rawlen = (uLongf)raw.size();
     if (uncompress(raw.data(), &rawlen, z.data(), (uLong)z.size()) != Z_OK || rawlen != raw.size())
@@ -807,7 +819,52 @@ void resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh)
     }
 }
 
+// ---- 8-bit PNG writer (gray or RGB, one IDAT, filter 0), zlib at best speed
+void put_chunk(std::vector<uint8_t> &png, const char *type, const std::vector<uint8_t> &data) {
+    const uint32_t n = (uint32_t)data.size();
+    const uint8_t len[4] = {(uint8_t)(n >> 24), (uint8_t)(n >> 16), (uint8_t)(n >> 8), (uint8_t)n};
+    png.insert(png.end(), len, len + 4);
+    const size_t start = png.size();
+    png.insert(png.end(), type, type + 4);
+    png.insert(png.end(), data.begin(), data.end());
+    const uLong crc = crc32(0L, png.data() + start, (uInt)(png.size() - start));
+    const uint8_t c[4] = {(uint8_t)(crc >> 24), (uint8_t)(crc >> 16), (uint8_t)(crc >> 8), (uint8_t)crc};
+    png.insert(png.end(), c, c + 4);
+}
+
+int write_png8(const char *path, int w, int h, int channels, const uint8_t *px) {
+    std::vector<uint8_t> raw;
+    raw.reserve((size_t)h * (channels * w + 1));
+    for (int y = 0; y < h; ++y) {
+        raw.push_back(0);
+        raw.insert(raw.end(), px + (size_t)y * channels * w, px + (size_t)(y + 1) * channels * w);
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), Z_BEST_SPEED) != Z_OK)
+        return ACMMP_ERR_IO;
+    z.resize(zlen);
+    std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::vector<uint8_t> ihdr = {(uint8_t)(w >> 24), (uint8_t)(w >> 16), (uint8_t)(w >> 8), (uint8_t)w,
+                                 (uint8_t)(h >> 24), (uint8_t)(h >> 16), (uint8_t)(h >> 8), (uint8_t)h,
+                                 8, (uint8_t)(channels == 3 ? 2 : 0), 0, 0, 0};
+    put_chunk(png, "IHDR", ihdr);
+    put_chunk(png, "IDAT", z);
+    put_chunk(png, "IEND", {});
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return ACMMP_ERR_IO;
+    const bool ok = std::fwrite(png.data(), 1, png.size(), f) == png.size();
+    std::fclose(f);
+    return ok ? ACMMP_OK : ACMMP_ERR_IO;
+}
+
 }  // namespace
+
+// triangulation.png (acmmp_pipeline.cpp) and the fusion's debug images
+int acmmp_internal_write_png(const char *path, int w, int h, int channels, const uint8_t *px) {
+    if (!path || !px || w <= 0 || h <= 0 || (channels != 1 && channels != 3)) return ACMMP_ERR_ARG;
+    return write_png8(path, w, h, channels, px);
+}
 
 extern "C" {
 

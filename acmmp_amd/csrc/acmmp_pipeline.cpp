@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/acmmp.hpp"
+#include "acmmp_hostio.h"
 
 namespace {
 
@@ -159,42 +160,10 @@ int write_dmb(const std::string &path, int h, int w, int nb, const float *data) 
 
 // ---- triangulation.png (src/acmmp_definitions.cpp:310-330): the reference
 // image as BGR with the triangle edges drawn in red, 1-px 8-connected lines.
-void put_chunk(std::vector<uint8_t> &png, const char *type, const std::vector<uint8_t> &data) {
-    const uint32_t n = (uint32_t)data.size();
-    const uint8_t len[4] = {(uint8_t)(n >> 24), (uint8_t)(n >> 16), (uint8_t)(n >> 8), (uint8_t)n};
-    png.insert(png.end(), len, len + 4);
-    const size_t start = png.size();
-    png.insert(png.end(), type, type + 4);
-    png.insert(png.end(), data.begin(), data.end());
-    const uLong crc = crc32(0L, png.data() + start, (uInt)(png.size() - start));
-    const uint8_t c[4] = {(uint8_t)(crc >> 24), (uint8_t)(crc >> 16), (uint8_t)(crc >> 8), (uint8_t)crc};
-    png.insert(png.end(), c, c + 4);
-}
-
 int write_png8(const std::string &path, int w, int h, int channels, const uint8_t *px) {
-    std::vector<uint8_t> raw;
-    raw.reserve((size_t)h * (channels * w + 1));
-    for (int y = 0; y < h; ++y) {
-        raw.push_back(0);
-        raw.insert(raw.end(), px + (size_t)y * channels * w, px + (size_t)(y + 1) * channels * w);
-    }
-    uLongf zlen = compressBound((uLong)raw.size());
-    std::vector<uint8_t> z(zlen);
-    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), Z_BEST_SPEED) != Z_OK)
-        return fail(ACMMP_ERR_IO, "zlib failed for %s", path.c_str());
-    z.resize(zlen);
-    std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
-    std::vector<uint8_t> ihdr = {(uint8_t)(w >> 24), (uint8_t)(w >> 16), (uint8_t)(w >> 8), (uint8_t)w,
-                                 (uint8_t)(h >> 24), (uint8_t)(h >> 16), (uint8_t)(h >> 8), (uint8_t)h,
-                                 8, (uint8_t)(channels == 3 ? 2 : 0), 0, 0, 0};
-    put_chunk(png, "IHDR", ihdr);
-    put_chunk(png, "IDAT", z);
-    put_chunk(png, "IEND", {});
-    FILE *f = std::fopen(path.c_str(), "wb");
-    if (!f) return fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
-    const bool ok = std::fwrite(png.data(), 1, png.size(), f) == png.size();
-    std::fclose(f);
-    return ok ? ACMMP_OK : fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    if (acmmp_internal_write_png(path.c_str(), w, h, channels, px))
+        return fail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    return ACMMP_OK;
 }
 
 void draw_line(std::vector<uint8_t> &rgb, int w, int h, acmmp::Point a, acmmp::Point b) {
@@ -344,11 +313,6 @@ void depth_normal_to_plane(float depth, float nx, float ny, float nz, int px, in
 
 }  // namespace
 
-// 8-bit grayscale PNG for the fusion's debug images (acmmp_fusion.cpp)
-int acmmp_internal_write_png_gray(const char *path, int w, int h, const uint8_t *px) {
-    return write_png8(path, w, h, 1, px);
-}
-
 extern "C" {
 
 int acmmp_priors_available(const char *dense_folder, int num_cams) {
@@ -421,8 +385,8 @@ int acmmp_generate_sample_list(const char *dense_folder, acmmp_problem *problems
         int num_src = 0;
         file >> pr.ref_image_id >> num_src;
         for (int j = 0; j < num_src; ++j) {
-            int id;
-            float score;
+            int id = 0;
+            float score = 0.0f;
             file >> id >> score;
             if (score <= 0.0f) continue;
             if (pr.num_src_images == ACMMP_MAX_IMAGES - 1)
