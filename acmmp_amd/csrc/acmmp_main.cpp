@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/acmmp.h"
+#include "acmmp_vp.h"
 
 namespace {
 
@@ -39,7 +40,12 @@ void usage() {
         "  --no_fusion              stop after the depth/normal/cost maps\n"
         "  --multi_fusion [DIR]     with -p: prior-aware fusion against <dense>DIR (default /ACMMP)\n"
         "  --force_fusion           prior-aware fusion even without -p\n"
-        "  --single_match_penalty N extra consistent views required of one-sided support (0)\n");
+        "  --single_match_penalty N extra consistent views required of one-sided support (0)\n"
+        "  --view_parallel          multi-GPU: one process per GPU (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/\n"
+        "                           MASTER_PORT from the environment, e.g. torchrun --no-python), views\n"
+        "                           sharded per pass, depth maps all-gathered (Jacobi order); rank 0 fuses\n"
+        "  --exchange rccl|tcp      view-parallel all-gather: RCCL (default) or TCP via the rendezvous\n"
+        "  --concurrent_views N     view-parallel: engines (HIP streams) per GPU (2)\n");
 }
 
 int die(const char *what) {
@@ -55,7 +61,8 @@ int main(int argc, char **argv) {
     bool multi_fusion = false, force_fusion = false;
     float consistency_scalar = 0.3f;
     int num_consistent_thresh = 1, single_match_penalty = 0;
-    int device = 0, iterations = 0;
+    int device = 0, iterations = 0, concurrent_views = 2;
+    bool device_set = false, view_parallel = false, exchange_rccl = true;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -76,6 +83,18 @@ int main(int argc, char **argv) {
             renamed_outdir = true;
         } else if (a == "--device") {
             device = std::atoi(value().c_str());
+            device_set = true;
+        } else if (a == "--view_parallel") {
+            view_parallel = true;
+        } else if (a == "--exchange") {
+            const std::string e = value();
+            if (e != "rccl" && e != "tcp") {
+                std::fprintf(stderr, "acmmp_main: --exchange rccl|tcp\n");
+                return 2;
+            }
+            exchange_rccl = e == "rccl";
+        } else if (a == "--concurrent_views") {
+            concurrent_views = std::atoi(value().c_str());
         } else if (a == "--iterations") {
             iterations = std::atoi(value().c_str());
         } else if (a == "--seed") {
@@ -157,6 +176,27 @@ int main(int argc, char **argv) {
     };
 
     const int geom_iterations = 2;
+    if (view_parallel) {
+        if (prior) {
+            std::fprintf(stderr, "acmmp_main: -p is not supported with --view_parallel\n");
+            return 2;
+        }
+        VpOptions vo;
+        vo.dense = dense_folder;
+        vo.output_dir = output_dir;
+        vo.device = device_set ? device : -1;
+        vo.iterations = iterations;
+        vo.seed = seed;
+        vo.geom_iterations = geom_iterations;
+        vo.concurrent_views = concurrent_views;
+        vo.exchange_rccl = exchange_rccl;
+        vo.verbose = !quiet;
+        const int rc = run_view_parallel(vo);
+        if (rc) return rc;
+        const char *r = std::getenv("RANK");
+        if (r && std::atoi(r) != 0) return 0;  // rank 0 fuses
+        max_num_downscale = -1;                 // the passes are done
+    }
     int flag = 0;
     while (max_num_downscale >= 0) {  // src/main_ACMMP.cpp:96-176
         if (!quiet) std::printf("Scale: %d\n", max_num_downscale);

@@ -1,0 +1,656 @@
+// acmmp_vp.cpp — view-parallel multi-GPU pass driver in C++,
+// `acmmp_main <dense> --view_parallel`: one process per GPU, the views of
+// every pass sharded over the ranks, depth maps exchanged with ONE RCCL
+// all-gather per pass. The same schedule as the Python driver
+// (acmmp_amd/distributed.py), so the .dmb outputs are bit-identical to it:
+//
+//   * sharding: LPT on W*H*(N-1) of the full-size reference image;
+//   * per scale (src/main_ACMMP.cpp:96-176): the images every owned view
+//     needs are decoded once (acmmp_load_view) and kept in HBM; the first
+//     scale runs the photometric + planar-prior pass, finer scales JBU +
+//     the hierarchy pass; then two geometric passes;
+//   * per view: the engine borrows the resident images
+//     (acmmp_set_images_device), the gathered depth maps and the view's
+//     previous state (acmmp_set_depth_maps_device /
+//     acmmp_set_plane_hypotheses_device) and exports its results
+//     device-to-device (acmmp_export_results); two engines per GPU, each
+//     on its own HIP stream, take views off a shared queue;
+//   * exchange: the depth maps of a pass go through a padded
+//     [world * slots, Hmax, Wmax] all-gather (ncclAllGather over xGMI, RCCL
+//     has no all-gatherv). Jacobi order: every view of a pass reads the
+//     previous pass's maps (the reference's second geometric pass is
+//     Gauss-Seidel, src/main_ACMMP.cpp:159-172; acmmp_main without
+//     --view_parallel keeps that order).
+//
+// Rendezvous: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR from the
+// environment (torchrun --no-python sets them); the ranks meet on TCP port
+// ACMMP_RDZV_PORT (default MASTER_PORT + 1, torchrun's own store holds
+// MASTER_PORT), where rank 0 hands out the ncclUniqueId. `--exchange tcp`
+// all-gathers through that socket instead (host staging: several ranks on
+// one GPU, where RCCL refuses duplicate devices — the 1-GPU parity tests).
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/acmmp.h"
+#include "acmmp_vp.h"
+
+namespace {
+
+struct Fail : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] void fail(const std::string &what) { throw Fail(what); }
+
+void hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) fail(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void acmmp_check(int rc, const char *what, const acmmp_ctx *ctx = nullptr) {
+    if (rc != ACMMP_OK)
+        fail(std::string(what) + " failed (status " + std::to_string(rc) + ")" +
+             (ctx ? std::string(": ") + acmmp_last_error(ctx) : std::string()));
+}
+
+// ------------------------------------------------------------ rendezvous
+// Rank 0 accepts world - 1 connections; each client announces its rank. The
+// sockets stay open for the id broadcast, barriers and the TCP exchange.
+void send_all(int fd, const void *p, size_t n) {
+    const char *c = static_cast<const char *>(p);
+    while (n) {
+        const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+        if (k <= 0) fail("rendezvous send failed");
+        c += k;
+        n -= (size_t)k;
+    }
+}
+
+void recv_all(int fd, void *p, size_t n) {
+    char *c = static_cast<char *>(p);
+    while (n) {
+        const ssize_t k = ::recv(fd, c, n, 0);
+        if (k <= 0) fail("rendezvous recv failed (peer gone)");
+        c += k;
+        n -= (size_t)k;
+    }
+}
+
+class Group {
+  public:
+    int rank = 0, world = 1;
+
+    Group(int rank_, int world_, const std::string &addr, int port) : rank(rank_), world(world_) {
+        if (world == 1) return;
+        if (rank == 0) {
+            const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+            const int one = 1;
+            ::setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+            sockaddr_in a{};
+            a.sin_family = AF_INET;
+            a.sin_port = htons((uint16_t)port);
+            a.sin_addr.s_addr = htonl(INADDR_ANY);
+            if (::bind(ls, (sockaddr *)&a, sizeof a) || ::listen(ls, world))
+                fail("rendezvous: cannot listen on port " + std::to_string(port));
+            peers_.assign(world, -1);
+            for (int k = 1; k < world; ++k) {
+                const int fd = ::accept(ls, nullptr, nullptr);
+                if (fd < 0) fail("rendezvous accept failed");
+                ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+                int32_t r = -1;
+                recv_all(fd, &r, sizeof r);
+                if (r <= 0 || r >= world || peers_[r] >= 0) fail("rendezvous: bad rank announcement");
+                peers_[r] = fd;
+            }
+            ::close(ls);
+        } else {
+            addrinfo hints{}, *res = nullptr;
+            hints.ai_family = AF_INET;
+            hints.ai_socktype = SOCK_STREAM;
+            if (::getaddrinfo(addr.c_str(), std::to_string(port).c_str(), &hints, &res) || !res)
+                fail("rendezvous: cannot resolve " + addr);
+            int fd = -1;
+            for (int attempt = 0; attempt < 600 && fd < 0; ++attempt) {  // rank 0 may start later: retry 60 s
+                fd = ::socket(AF_INET, SOCK_STREAM, 0);
+                if (::connect(fd, res->ai_addr, res->ai_addrlen)) {
+                    ::close(fd);
+                    fd = -1;
+                    ::usleep(100000);
+                }
+            }
+            ::freeaddrinfo(res);
+            if (fd < 0) fail("rendezvous: cannot connect to " + addr + ":" + std::to_string(port));
+            const int one = 1;
+            ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+            const int32_t r = rank;
+            send_all(fd, &r, sizeof r);
+            root_ = fd;
+        }
+    }
+
+    ~Group() {
+        for (int fd : peers_)
+            if (fd >= 0) ::close(fd);
+        if (root_ >= 0) ::close(root_);
+    }
+
+    // rank 0's bytes to every rank
+    void broadcast(void *p, size_t n) {
+        if (world == 1) return;
+        if (rank == 0)
+            for (int k = 1; k < world; ++k) send_all(peers_[k], p, n);
+        else
+            recv_all(root_, p, n);
+    }
+
+    // every rank's n bytes, concatenated in rank order, to every rank
+    void allgather(const void *mine, void *all, size_t n) {
+        char *out = static_cast<char *>(all);
+        std::memcpy(out + (size_t)rank * n, mine, n);
+        if (world == 1) return;
+        if (rank == 0) {
+            for (int k = 1; k < world; ++k) recv_all(peers_[k], out + (size_t)k * n, n);
+            for (int k = 1; k < world; ++k) send_all(peers_[k], out, (size_t)world * n);
+        } else {
+            send_all(root_, mine, n);
+            recv_all(root_, out, (size_t)world * n);
+        }
+    }
+
+    void barrier() {
+        char b = 0;
+        std::vector<char> all((size_t)world);
+        allgather(&b, all.data(), 1);
+    }
+
+  private:
+    std::vector<int> peers_;
+    int root_ = -1;
+};
+
+// ------------------------------------------------------------ exchange
+class Exchange {
+  public:
+    Exchange(Group &g, bool rccl, int device) : g_(g), rccl_(rccl) {
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+        if (rccl_) {
+            ncclUniqueId id;
+            if (g.rank == 0 && ncclGetUniqueId(&id) != ncclSuccess) fail("ncclGetUniqueId failed");
+            g.broadcast(&id, sizeof id);
+            const ncclResult_t r = ncclCommInitRank(&comm_, g.world, id, g.rank);
+            if (r != ncclSuccess) fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    ~Exchange() {
+        if (comm_) ncclCommDestroy(comm_);
+        if (stream_) (void)hipStreamDestroy(stream_);
+    }
+
+    // d_recv[world * count] = concatenation of every rank's d_send[count]
+    void allgather(const float *d_send, float *d_recv, size_t count) {
+        if (rccl_) {  // world 1 included: the same RCCL call as at 8 GPUs
+            const ncclResult_t r = ncclAllGather(d_send, d_recv, count, ncclFloat32, comm_, stream_);
+            if (r != ncclSuccess) fail(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        } else if (g_.world == 1) {
+            hip_check(hipMemcpyAsync(d_recv, d_send, count * sizeof(float), hipMemcpyDeviceToDevice, stream_),
+                      "hipMemcpyAsync");
+        } else {
+            std::vector<float> mine(count), all(count * (size_t)g_.world);
+            hip_check(hipMemcpy(mine.data(), d_send, count * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+            g_.allgather(mine.data(), all.data(), count * sizeof(float));
+            hip_check(hipMemcpy(d_recv, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
+        }
+        // the engines' streams do not wait on this one
+        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    }
+
+  private:
+    Group &g_;
+    bool rccl_;
+    ncclComm_t comm_ = nullptr;
+    hipStream_t stream_ = nullptr;
+};
+
+// ------------------------------------------------------------ buffers
+struct DevBuf {
+    float *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) : n(count) {
+        if (count) hip_check(hipMalloc((void **)&p, count * sizeof(float)), "hipMalloc");
+    }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        return *this;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+std::string image_path(const std::string &dense, int id) {
+    char name[32];
+    std::snprintf(name, sizeof name, "%08d", id);
+    const std::string base = dense + "/images/" + name;
+    for (const char *ext : {".jpg", ".pgm", ".pfm"}) {
+        struct stat st;
+        if (::stat((base + ext).c_str(), &st) == 0) return base + ext;
+    }
+    return base + ".jpg";
+}
+
+std::string result_folder(const std::string &out, int ref_id) {
+    char name[32];
+    std::snprintf(name, sizeof name, "/2333_%08d", ref_id);
+    return out + name;
+}
+
+struct ViewState {
+    DevBuf planes, costs;  // (H, W, 4) world normal + depth, (H, W)
+    int W = 0, H = 0;
+    std::vector<float> jbu;  // upsampled depth of the hierarchy pass (host)
+};
+
+// --------------------------------------------------------------- driver
+class Driver {
+  public:
+    Driver(const VpOptions &o, Group &g) : o_(o), g_(g), ex_(g, o.exchange_rccl, o.device) {
+        output_folder_ = o.dense + o.output_dir;
+        problems_.resize(4096);
+        int n = 0;
+        acmmp_check(acmmp_generate_sample_list(o.dense.c_str(), problems_.data(), (int)problems_.size(), &n),
+                    "GenerateSampleList");
+        problems_.resize((size_t)n);
+        acmmp_check(acmmp_compute_multiscale_settings(o.dense.c_str(), problems_.data(), n, &max_down_),
+                    "ComputeMultiScaleSettings");
+        for (int i = 0; i < n; ++i) index_of_[problems_[(size_t)i].ref_image_id] = i;
+        // LPT on W*H*max(N-1, 1) of the full-size reference image
+        std::vector<double> cost((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            int w = 0, h = 0;
+            acmmp_check(acmmp_image_size(image_path(o.dense, problems_[(size_t)i].ref_image_id).c_str(), &w, &h),
+                        "image header");
+            cost[(size_t)i] = (double)w * h * std::max(problems_[(size_t)i].num_src_images, 1);
+        }
+        std::vector<int> order((size_t)n);
+        for (int i = 0; i < n; ++i) order[(size_t)i] = i;
+        std::sort(order.begin(), order.end(), [&](int a, int b) {
+            return cost[(size_t)a] != cost[(size_t)b] ? cost[(size_t)a] > cost[(size_t)b] : a < b;
+        });
+        std::vector<double> load((size_t)g.world, 0.0);
+        assignment_.assign((size_t)g.world, {});
+        for (int v : order) {
+            int r = 0;
+            for (int k = 1; k < g.world; ++k)
+                if (load[(size_t)k] < load[(size_t)r]) r = k;
+            assignment_[(size_t)r].push_back(v);
+            load[(size_t)r] += cost[(size_t)v];
+        }
+        for (auto &a : assignment_) std::sort(a.begin(), a.end());
+        mine_ = assignment_[(size_t)g.rank];
+        for (int k = 0; k < std::max(o.concurrent_views, 1); ++k) {
+            acmmp_ctx *ctx = nullptr;
+            acmmp_check(acmmp_create(o.device, &ctx), "acmmp_create");
+            engines_.push_back(ctx);
+        }
+    }
+
+    ~Driver() {
+        for (auto *e : engines_) acmmp_destroy(e);
+    }
+
+    void run() {
+        ::mkdir(output_folder_.c_str(), 0777);
+        bool first = true;
+        while (max_down_ >= 0) {
+            for (auto &p : problems_)  // cur_image_size for this scale (src/main_ACMMP.cpp:99-106)
+                if (p.num_downscale >= 0) {
+                    p.cur_image_size = (int)(p.max_image_size / std::pow(2.0, p.num_downscale));
+                    p.num_downscale--;
+                }
+            load_views();
+            shapes();
+            if (first) {
+                first = false;
+                run_pass(false, true, false, false);
+            } else {
+                jbu();
+                run_pass(false, true, true, false);
+            }
+            for (int gi = 0; gi < o_.geom_iterations; ++gi) run_pass(true, false, false, gi > 0);
+            max_down_--;
+        }
+        g_.barrier();
+    }
+
+  private:
+    struct Task {
+        int v;  // problem index
+        bool geom, planar, hier, multi;
+    };
+
+    void load_views() {
+        images_.clear();
+        cams_.clear();
+        host_images_.clear();
+        std::vector<int> need;
+        for (int v : mine_) {
+            const acmmp_problem &p = problems_[(size_t)v];
+            need.push_back(p.ref_image_id);
+            for (int s = 0; s < p.num_src_images; ++s) need.push_back(p.src_image_ids[s]);
+        }
+        std::sort(need.begin(), need.end());
+        need.erase(std::unique(need.begin(), need.end()), need.end());
+        std::vector<std::vector<float>> host(need.size());
+        std::vector<acmmp_camera> cams(need.size());
+        std::vector<std::string> errs(need.size());
+        std::atomic<size_t> next{0};
+        auto worker = [&]() {
+            for (size_t k; (k = next++) < need.size();) {
+                const int id = need[k];
+                auto it = index_of_.find(id);
+                if (it == index_of_.end()) {
+                    errs[k] = "source id " + std::to_string(id) + " is not a problem index";
+                    continue;
+                }
+                const int size = problems_[(size_t)it->second].cur_image_size;
+                int rc = acmmp_load_view(o_.dense.c_str(), id, size, nullptr, 0, &cams[k]);
+                if (rc != ACMMP_OK && rc != ACMMP_ERR_ARG) {
+                    errs[k] = std::string("acmmp_load_view: ") + acmmp_pipeline_last_error();
+                    continue;
+                }
+                host[k].resize((size_t)cams[k].width * cams[k].height);
+                rc = acmmp_load_view(o_.dense.c_str(), id, size, host[k].data(), host[k].size(), &cams[k]);
+                if (rc != ACMMP_OK) errs[k] = std::string("acmmp_load_view: ") + acmmp_pipeline_last_error();
+            }
+        };
+        std::vector<std::thread> pool;
+        const int nt = (int)std::min<size_t>(16, need.size());
+        for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+        for (auto &t : pool) t.join();
+        for (size_t k = 0; k < need.size(); ++k)
+            if (!errs[k].empty()) fail("view " + std::to_string(need[k]) + ": " + errs[k]);
+        for (size_t k = 0; k < need.size(); ++k) {
+            DevBuf d(host[k].size());
+            hip_check(hipMemcpy(d.p, host[k].data(), host[k].size() * sizeof(float), hipMemcpyHostToDevice),
+                      "hipMemcpy");
+            images_.emplace(need[k], std::move(d));
+            cams_[need[k]] = cams[k];
+            host_images_[need[k]] = std::move(host[k]);
+        }
+    }
+
+    // (h, w) of every view at this scale (acmmp_load_view's rescale rule)
+    void shapes() {
+        shape_.assign(problems_.size(), {0, 0});
+        int hmax = 0, wmax = 0;
+        for (size_t i = 0; i < problems_.size(); ++i) {
+            int w = 0, h = 0;
+            acmmp_check(acmmp_image_size(image_path(o_.dense, problems_[i].ref_image_id).c_str(), &w, &h),
+                        "image header");
+            const int m = problems_[i].cur_image_size;
+            if (w > m || h > m) {
+                const float f = std::min((float)m / (float)w, (float)m / (float)h);
+                w = (int)std::nearbyint((float)w * f);
+                h = (int)std::nearbyint((float)h * f);
+            }
+            shape_[i] = {h, w};
+            hmax = std::max(hmax, h);
+            wmax = std::max(wmax, w);
+        }
+        slots_ = 1;
+        for (auto &a : assignment_) slots_ = std::max(slots_, (int)a.size());
+        hmax_ = hmax;
+        wmax_ = wmax;
+        const size_t per = (size_t)slots_ * hmax_ * wmax_;
+        send_ = DevBuf(per);
+        recv_ = DevBuf(per * (size_t)g_.world);
+        depth_tmp_.clear();
+    }
+
+    acmmp_params view_params(const Task &t) const {
+        acmmp_params p;
+        acmmp_default_params(&p);
+        if (t.geom) {  // SetGeomConsistencyParams (src/ACMMP.cpp:447-454)
+            p.geom_consistency = 1;
+            p.max_iterations = 2;
+            if (t.multi) p.multi_geometry = 1;
+        }
+        if (t.hier) p.hierarchy = 1;
+        const acmmp_problem &pr = problems_[(size_t)t.v];
+        p.seed_lo = o_.seed + (unsigned)pr.ref_image_id;
+        p.seed_hi = (unsigned)pass_index_;
+        if (o_.iterations > 0) p.max_iterations = o_.iterations;
+        return p;
+    }
+
+    // the gathered depth map of problem i (previous pass) and its pitch
+    const float *gathered(int i) const {
+        for (int r = 0; r < g_.world; ++r) {
+            const auto &a = assignment_[(size_t)r];
+            for (size_t k = 0; k < a.size(); ++k)
+                if (a[k] == i) return recv_.p + ((size_t)r * slots_ + k) * hmax_ * wmax_;
+        }
+        fail("view not assigned");
+    }
+
+    void compute(acmmp_ctx *eng, const Task &t, ViewState &out) {
+        const acmmp_problem &pr = problems_[(size_t)t.v];
+        std::vector<int> ids = {pr.ref_image_id};
+        for (int s = 0; s < pr.num_src_images; ++s) ids.push_back(pr.src_image_ids[s]);
+        std::vector<acmmp_camera> cams;
+        std::vector<const float *> imgs;
+        for (int id : ids) {
+            cams.push_back(cams_.at(id));
+            imgs.push_back(images_.at(id).p);
+        }
+        const acmmp_params p = view_params(t);
+        acmmp_check(acmmp_set_params(eng, &p), "acmmp_set_params", eng);
+        acmmp_check(acmmp_set_images_device(eng, (int)ids.size(), cams.data(), imgs.data(), nullptr, 0),
+                    "acmmp_set_images_device", eng);
+        const int W = cams[0].width, H = cams[0].height;
+        ViewState &prev = state_[t.v];
+        if (t.geom) {
+            std::vector<const float *> deps;
+            std::vector<int32_t> pitches;
+            for (int id : ids) {
+                deps.push_back(gathered(index_of_.at(id)));
+                pitches.push_back(wmax_);
+            }
+            acmmp_check(acmmp_set_depth_maps_device(eng, deps.data(), pitches.data()), "acmmp_set_depth_maps_device",
+                        eng);
+            acmmp_check(acmmp_set_plane_hypotheses_device(eng, prev.planes.p, prev.costs.p),
+                        "acmmp_set_plane_hypotheses_device", eng);
+        }
+        if (t.hier) {  // scaled planes = previous scale's normals + (costs, or the JBU depth when no upsample)
+            const int sh = prev.H, sw = prev.W;
+            std::vector<float> pl((size_t)sh * sw * 4), co((size_t)sh * sw);
+            hip_check(hipMemcpy(pl.data(), prev.planes.p, pl.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+            hip_check(hipMemcpy(co.data(), prev.costs.p, co.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+            const bool upsample = sw != H || sh != W;  // src/ACMMP.cpp:766, rows/cols swap included
+            std::vector<float> scaled(pl.size());
+            for (size_t k = 0; k < (size_t)sh * sw; ++k) {
+                scaled[4 * k + 0] = pl[4 * k + 0];
+                scaled[4 * k + 1] = pl[4 * k + 1];
+                scaled[4 * k + 2] = pl[4 * k + 2];
+                scaled[4 * k + 3] = upsample ? co[k] : prev.jbu[k];
+            }
+            acmmp_check(acmmp_set_hierarchy_inputs(eng, scaled.data(), sw, sh, prev.jbu.data()),
+                        "acmmp_set_hierarchy_inputs", eng);
+        }
+        acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
+        if (t.planar) {
+            acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+            int nsp = 0, ntri = 0;
+            acmmp_check(acmmp_prepare_planar_prior(eng, &nsp, &ntri), "acmmp_prepare_planar_prior", eng);
+            acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
+        }
+        out.W = W;
+        out.H = H;
+        out.planes = DevBuf((size_t)W * H * 4);
+        out.costs = DevBuf((size_t)W * H);
+        DevBuf depth((size_t)W * H);
+        acmmp_check(acmmp_export_results(eng, out.planes.p, out.costs.p, depth.p), "acmmp_export_results", eng);
+        acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+        std::lock_guard<std::mutex> lk(mu_);
+        depth_tmp_[t.v] = std::move(depth);
+    }
+
+    void write_outputs(int v, const ViewState &s, bool geom) {
+        const std::string folder = result_folder(output_folder_, problems_[(size_t)v].ref_image_id);
+        ::mkdir(folder.c_str(), 0777);
+        const size_t P = (size_t)s.W * s.H;
+        std::vector<float> pl(P * 4), co(P), d(P), n(P * 3);
+        hip_check(hipMemcpy(pl.data(), s.planes.p, pl.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_check(hipMemcpy(co.data(), s.costs.p, co.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+        for (size_t k = 0; k < P; ++k) {
+            d[k] = pl[4 * k + 3];
+            n[3 * k + 0] = pl[4 * k + 0];
+            n[3 * k + 1] = pl[4 * k + 1];
+            n[3 * k + 2] = pl[4 * k + 2];
+        }
+        const std::string dn = folder + (geom ? "/depths_geom.dmb" : "/depths.dmb");
+        if (acmmp_write_dmb(dn.c_str(), s.H, s.W, 1, d.data()) ||
+            acmmp_write_dmb((folder + "/normals.dmb").c_str(), s.H, s.W, 3, n.data()) ||
+            acmmp_write_dmb((folder + "/costs.dmb").c_str(), s.H, s.W, 1, co.data()))
+            fail("cannot write the .dmb outputs of view " + std::to_string(problems_[(size_t)v].ref_image_id));
+    }
+
+    void run_pass(bool geom, bool planar, bool hier, bool multi) {
+        std::vector<Task> tasks;
+        for (int v : mine_) tasks.push_back({v, geom, planar, hier, multi});
+        std::map<int, ViewState> next;
+        for (int v : mine_) {  // every key exists before the worker threads look them up
+            next[v];
+            state_[v];
+        }
+        // views off a shared queue, one host thread per engine
+        std::atomic<size_t> q{0};
+        std::vector<std::string> errs(engines_.size());
+        auto worker = [&](size_t e) {
+            try {
+                hip_check(hipSetDevice(o_.device), "hipSetDevice");  // per thread: the output buffers go there
+                for (size_t k; (k = q++) < tasks.size();) compute(engines_[e], tasks[k], next[tasks[k].v]);
+            } catch (const std::exception &ex) {
+                errs[e] = ex.what();
+                q = tasks.size();
+            }
+        };
+        std::vector<std::thread> th;
+        for (size_t e = 0; e < engines_.size(); ++e) th.emplace_back(worker, e);
+        for (auto &t : th) t.join();
+        for (auto &e : errs)
+            if (!e.empty()) fail(e);
+        // state, outputs (view order), then the padded all-gather of the depth maps
+        hip_check(hipMemset(send_.p, 0, send_.n * sizeof(float)), "hipMemset");
+        for (size_t k = 0; k < mine_.size(); ++k) {
+            const int v = mine_[k];
+            ViewState &s = next[v];
+            if (o_.write_outputs) write_outputs(v, s, geom);
+            hip_check(hipMemcpy2D(send_.p + k * (size_t)hmax_ * wmax_, (size_t)wmax_ * sizeof(float),
+                                  depth_tmp_.at(v).p, (size_t)s.W * sizeof(float), (size_t)s.W * sizeof(float),
+                                  (size_t)s.H, hipMemcpyDeviceToDevice),
+                      "hipMemcpy2D");
+            state_[v] = std::move(s);
+        }
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        depth_tmp_.clear();
+        ex_.allgather(send_.p, recv_.p, send_.n);
+        pass_index_++;
+    }
+
+    // JointBilateralUpsampling of each owned view's previous-scale depth to
+    // this scale's image (src/ACMMP.cpp:964-1087), kept for the hierarchy pass
+    void jbu() {
+        for (int v : mine_) {
+            ViewState &s = state_[v];
+            const int id = problems_[(size_t)v].ref_image_id;
+            const acmmp_camera &c = cams_.at(id);
+            const std::vector<float> &img = host_images_.at(id);
+            const size_t P = (size_t)s.W * s.H;
+            std::vector<float> pl(P * 4), d(P);
+            hip_check(hipMemcpy(pl.data(), s.planes.p, pl.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+            for (size_t k = 0; k < P; ++k) d[k] = pl[4 * k + 3];
+            s.jbu.assign((size_t)c.width * c.height, 0.0f);
+            int isc = 0;
+            acmmp_check(acmmp_joint_bilateral_upsample(o_.device, img.data(), c.width, c.height, d.data(), s.W, s.H,
+                                                       s.jbu.data(), &isc),
+                        "acmmp_joint_bilateral_upsample");
+            if (isc <= 1) fail("view " + std::to_string(id) + ": JBU image scale 1 (nothing to upsample)");
+        }
+    }
+
+    VpOptions o_;
+    Group &g_;
+    Exchange ex_;
+    std::string output_folder_;
+    std::vector<acmmp_problem> problems_;
+    std::map<int, int> index_of_;
+    int max_down_ = -1;
+    std::vector<std::vector<int>> assignment_;
+    std::vector<int> mine_;
+    std::vector<acmmp_ctx *> engines_;
+    std::map<int, DevBuf> images_;
+    std::map<int, acmmp_camera> cams_;
+    std::map<int, std::vector<float>> host_images_;
+    std::vector<std::pair<int, int>> shape_;
+    int slots_ = 1, hmax_ = 0, wmax_ = 0;
+    DevBuf send_, recv_;
+    std::map<int, DevBuf> depth_tmp_;
+    std::map<int, ViewState> state_;
+    std::mutex mu_;
+    int pass_index_ = 0;
+};
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+}  // namespace
+
+int run_view_parallel(const VpOptions &opt) {
+    try {
+        const int rank = env_int("RANK", 0), world = env_int("WORLD_SIZE", 1);
+        VpOptions o = opt;
+        if (o.device < 0) o.device = env_int("LOCAL_RANK", 0);
+        const char *addr = std::getenv("MASTER_ADDR");
+        const int port = env_int("ACMMP_RDZV_PORT", env_int("MASTER_PORT", 29500) + 1);
+        if (rank < 0 || world < 1 || rank >= world) fail("bad RANK / WORLD_SIZE");
+        Group g(rank, world, addr && *addr ? addr : "127.0.0.1", port);
+        Driver d(o, g);
+        d.run();
+        if (rank == 0 && o.verbose)
+            std::printf("view-parallel: %d ranks (%s exchange), maps under %s%s\n", world,
+                        o.exchange_rccl ? "RCCL" : "TCP", o.dense.c_str(), o.output_dir.c_str());
+        return 0;
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "acmmp_main --view_parallel: %s\n", e.what());
+        return 1;
+    }
+}

@@ -38,9 +38,17 @@ __global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, i
             case 4: h = h * 1664525u + 1013904223u; idx = (int)(h % (unsigned)nrec); break;  // random
             case 5: idx = base + (s & 7); break;                                        // broadcast
             case 6: idx = base + r * PITCH * 2 + 2 * c + (s % 6) * 2; break;            // rows 2 apart
+            case 8: case 9: case 10: case 11:                                          // k_sweep shape, 1/4 / 1/16 / 1 lane / 1/2 active
+                idx = base + r * PITCH + 2 * c + (s % 6) * 2 + (s / 6) * 2 * PITCH; break;
+            case 12: h = h * 1664525u + 1013904223u; idx = (int)(h % (unsigned)nrec); break;  // random, 1/4 active
             default: idx = base + lane * 33; break;                                     // one line per lane
         }
-        acc += sbl32(rs, idx, 0, 0, 0);
+        const bool on = pattern == 8 || pattern == 12 ? (lane & 3) == 0
+                        : pattern == 9                ? (lane & 15) == 0
+                        : pattern == 10               ? lane == 0
+                        : pattern == 11               ? (lane & 1) == 0
+                                                      : true;
+        if (on) acc += sbl32(rs, idx, 0, 0, 0);
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -55,7 +63,7 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int p = 0; p < 8; ++p) {
+    for (int p = 0; p < 13; ++p) {
         for (int rep = 0; rep < 3; ++rep) {
             (void)hipEventRecord(a);
             k_gather<<<blocks, 256>>>(buf, nrec, p, out);

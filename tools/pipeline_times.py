@@ -16,7 +16,7 @@ Synthetic, seeded scene rendered on the GPU and written as 8-bit JPEGs (a
 COLMAP-converted dense folder); wall times include JPEG decode and .dmb I/O,
 as the reference's do. Iterations: the driver's default (the reference's).
 usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] [steps] > gpurun_out/pipeline.jsonl
-  steps: comma list of distributed,cli,fusion (default all; fusion needs cli)
+  steps: comma list of distributed,cli_vp,cli,fusion (default distributed,cli,fusion; fusion needs cli)
 """
 import json
 import os
@@ -74,6 +74,16 @@ def main():
              gpu_runpatchmatch_s=round(pipe.gpu_ms / 1e3, 2),
              phases_s={k: round(v, 2) for k, v in sorted(pipe.phase_s.items())})
         shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
+    if "cli_vp" in STEPS:  # the C++ view-parallel driver, world 1 through RCCL
+        cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
+        env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT="29611")
+        t0 = time.perf_counter()
+        subprocess.run([cli, dense, "--view_parallel", "--output_dir", "/ACMMP_cvp", "--no_fusion", "--quiet"],
+                       stdout=sys.stderr, check=True, env=env)
+        emit(step="cli_view_parallel_world1", order="jacobi", concurrent_views=2, exchange="rccl",
+             s=round(time.perf_counter() - t0, 2))
+        shutil.rmtree(dense + "/ACMMP_cvp", ignore_errors=True)
     if "cli" not in STEPS:
         shutil.rmtree(tmp, ignore_errors=True)
         return
