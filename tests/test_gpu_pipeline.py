@@ -91,3 +91,25 @@ def test_seeded_pipeline_matches_oracle(tmp_path):
     assert out.endswith("/ACMMP_PRIOR")
     maps = OraclePipeline(d).run_single_scale("sequential", priors=priors)
     assert _compare(out, maps) == 4 * 4
+
+
+def test_cli_fusion_of_gpu_maps_matches_restatement(dense):
+    """RunFusion (src/acmmp_definitions.cpp:828-1043) over the maps the GPU
+    passes wrote: the C++ CLI's PLY against the Python restatement
+    (tests/oracle_fusion.py) over the same maps, record for record,
+    bit-exact. Record order: the reference writes its PLY records from an
+    `omp parallel for` with an `omp critical` fwrite (src/ACMMP.cpp:405-432),
+    i.e. in a nondeterministic order; ours keep the fusion's own point order
+    (pixel order of each view, views in pair.txt order), so a reference PLY of
+    the same maps equals ours as a multiset of records."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle_fusion import read_ply, run_fusion
+    from test_fusion import _compare_cloud
+    exe = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
+    r = subprocess.run([exe, dense, "--output_dir", "/CLIF", "--quiet"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ply = read_ply(os.path.join(dense + "/CLIF", "ACMMP_model.ply"))
+    ref = run_fusion(dense, dense + "/CLIF")
+    assert len(ref) > 1000
+    _compare_cloud(ply, ref)
