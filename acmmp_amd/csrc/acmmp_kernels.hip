@@ -55,6 +55,10 @@ constexpr int kTaps = 6;
 #ifndef ACMMP_PIPE_ROWS
 #define ACMMP_PIPE_ROWS 1
 #endif
+// view selection's CDF and the photometric final costs with static indices
+#ifndef ACMMP_SELECT_REGS
+#define ACMMP_SELECT_REGS 1
+#endif
 // Minimum waves per SIMD the sweep kernel is register-allocated for
 // (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
 #ifndef ACMMP_SWEEP_WAVES
@@ -1418,6 +1422,44 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
 
     DIAG_T(t_phaseA);
     // ---- multi-hypothesis joint view selection (:994-1056)
+#if ACMMP_SELECT_REGS
+    // CDF in registers (static indices over NS, predicated on i < nsrc): the
+    // 15 draws then need no dependent scratch loads. The CDF is
+    // nondecreasing (non-negative terms; once NaN it stays NaN), so the
+    // reference's "first i with cdf[i] > r" (:1036-1041) is the count of
+    // entries <= r, taken only if that entry is > r (a NaN or all-<= r CDF
+    // selects nothing, as in the reference).
+    float cdf[NS];
+    {  // TransformPDFToCDF (:107-121), same operations and order
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            cdf[i] = i < nsrc ? probs[i] : 0.0f;
+            if (i < nsrc) sum += cdf[i];
+        }
+        const float inv = 1.0f / sum;
+        float cum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            if (i < nsrc) {
+                cum += cdf[i] * inv;
+                cdf[i] = cum;
+            }
+    }
+    dm_rng rs = make_rng(kv, center, 1u + (uint32_t)iter);
+    ViewCounts vw;
+#pragma unroll 1
+    for (int sample = 0; sample < 15; ++sample) {
+        const float rand_prob = dm_rng_uniform(&rs) - FLT_EPSILON;
+        int idx = 0;
+        float at = cdf[0];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) idx += (i < nsrc && cdf[i] <= rand_prob) ? 1 : 0;
+#pragma unroll
+        for (int i = 1; i < NS; ++i) at = idx == i ? cdf[i] : at;
+        if (idx < nsrc && at > rand_prob) vw.add(idx);
+    }
+#else
     {  // TransformPDFToCDF (:107-121)
         float sum = 0.0f;
         for (int i = 0; i < nsrc; ++i) sum += probs[i];
@@ -1436,6 +1478,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
             if (probs[image_id] > rand_prob) { vw.add(image_id); break; }
         }
     }
+#endif
     uint32_t temp_sv = 0;
     float weight_norm = 0;
     for (int i = 0; i < nsrc; ++i) {
@@ -1453,6 +1496,24 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     }
 #endif
     float final_costs[8];
+#if ACMMP_SELECT_REGS
+    if (!prm.geom_consistency) {
+        // photometric: the NS cost loads of a candidate issued together
+        // (static offsets), unsampled views add +0 (costs are finite and
+        // >= 0, fc >= +0: the same sum as skipping them)
+        for (int i = 0; i < 8; ++i) {
+            float fc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NS; ++j)
+                if (j < nsrc) {
+                    const float wj = (float)vw.get(j);
+                    const float cj = cost_array[i][j];
+                    fc += wj > 0 ? wj * cj : 0.0f;
+                }
+            final_costs[i] = fc / weight_norm;
+        }
+    } else
+#endif
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
         const bool fl = (flags >> i) & 1u;
