@@ -41,6 +41,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -321,6 +322,8 @@ class Driver {
     }
 
     ~Driver() {
+        for (auto &t : writers_)
+            if (t.joinable()) t.join();
         for (auto *e : engines_) acmmp_destroy(e);
     }
 
@@ -333,19 +336,34 @@ class Driver {
                     p.cur_image_size = (int)(p.max_image_size / std::pow(2.0, p.num_downscale));
                     p.num_downscale--;
                 }
-            load_views();
-            shapes();
+            {
+                Clock c(this, "load");
+                load_views();
+                shapes();
+            }
             if (first) {
                 first = false;
                 run_pass(false, true, false, false);
             } else {
-                jbu();
+                {
+                    Clock c(this, "jbu");
+                    jbu();
+                }
                 run_pass(false, true, true, false);
             }
             for (int gi = 0; gi < o_.geom_iterations; ++gi) run_pass(true, false, false, gi > 0);
             max_down_--;
         }
+        {
+            Clock c(this, "flush_writes");
+            flush_writes();
+        }
         g_.barrier();
+        if (std::getenv("ACMMP_HOST_TIMING")) {
+            std::fprintf(stderr, "[rank %d]", g_.rank);
+            for (auto &kv : phase_s_) std::fprintf(stderr, " %s=%.2fs", kv.first.c_str(), kv.second);
+            std::fprintf(stderr, "\n");
+        }
     }
 
   private:
@@ -353,6 +371,43 @@ class Driver {
         int v;  // problem index
         bool geom, planar, hier, multi;
     };
+
+    // wall seconds per phase (ACMMP_HOST_TIMING=1 prints them)
+    struct Clock {
+        Driver *d;
+        const char *name;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+        Clock(Driver *d_, const char *n) : d(d_), name(n) {}
+        ~Clock() {
+            d->phase_s_[name] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+    };
+
+    // the .dmb writers of the previous pass have finished (they read the
+    // state buffers the next pass end replaces); their first error is raised
+    void flush_writes() {
+        for (auto &t : writers_) t.join();
+        writers_.clear();
+        for (auto &e : write_errs_)
+            if (!e.empty()) fail(e);
+        write_errs_.clear();
+    }
+
+    // a pass's outputs written by 4 host threads while the next pass computes
+    void start_writes(bool geom) {
+        const int nw = (int)std::min<size_t>(4, mine_.size());
+        write_errs_.assign((size_t)nw, std::string());
+        for (int w = 0; w < nw; ++w)
+            writers_.emplace_back([this, w, nw, geom]() {
+                try {
+                    hip_check(hipSetDevice(o_.device), "hipSetDevice");
+                    for (size_t k = (size_t)w; k < mine_.size(); k += (size_t)nw)
+                        write_outputs(mine_[k], state_.at(mine_[k]), geom);
+                } catch (const std::exception &e) {
+                    write_errs_[(size_t)w] = e.what();
+                }
+            });
+    }
 
     void load_views() {
         images_.clear();
@@ -561,17 +616,25 @@ class Driver {
                 q = tasks.size();
             }
         };
-        std::vector<std::thread> th;
-        for (size_t e = 0; e < engines_.size(); ++e) th.emplace_back(worker, e);
-        for (auto &t : th) t.join();
+        {
+            Clock c(this, "compute");
+            std::vector<std::thread> th;
+            for (size_t e = 0; e < engines_.size(); ++e) th.emplace_back(worker, e);
+            for (auto &t : th) t.join();
+        }
         for (auto &e : errs)
             if (!e.empty()) fail(e);
-        // state, outputs (view order), then the padded all-gather of the depth maps
+        {
+            Clock c(this, "flush_writes");
+            flush_writes();  // the previous pass's writers still read the state replaced below
+        }
+        Clock c(this, "exchange");
+        // state, then the padded all-gather of the depth maps; the outputs are
+        // written while the next pass computes
         hip_check(hipMemset(send_.p, 0, send_.n * sizeof(float)), "hipMemset");
         for (size_t k = 0; k < mine_.size(); ++k) {
             const int v = mine_[k];
             ViewState &s = next[v];
-            if (o_.write_outputs) write_outputs(v, s, geom);
             hip_check(hipMemcpy2D(send_.p + k * (size_t)hmax_ * wmax_, (size_t)wmax_ * sizeof(float),
                                   depth_tmp_.at(v).p, (size_t)s.W * sizeof(float), (size_t)s.W * sizeof(float),
                                   (size_t)s.H, hipMemcpyDeviceToDevice),
@@ -580,6 +643,7 @@ class Driver {
         }
         hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
         depth_tmp_.clear();
+        if (o_.write_outputs) start_writes(geom);
         ex_.allgather(send_.p, recv_.p, send_.n);
         pass_index_++;
     }
@@ -625,6 +689,9 @@ class Driver {
     std::map<int, ViewState> state_;
     std::mutex mu_;
     int pass_index_ = 0;
+    std::vector<std::thread> writers_;
+    std::vector<std::string> write_errs_;
+    std::map<std::string, double> phase_s_;
 };
 
 int env_int(const char *name, int dflt) {
