@@ -65,7 +65,8 @@ class Params(C.Structure):
         ("seed_lo", C.c_uint32),
         ("seed_hi", C.c_uint32),
         ("rng_stream", C.c_uint32),
-        ("reserved", C.c_int32 * 5),
+        ("texture_filter8", C.c_int32),
+        ("reserved", C.c_int32 * 4),
     ]
 
 

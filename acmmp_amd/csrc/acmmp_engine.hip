@@ -630,6 +630,8 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
+    if (p.texture_filter8 && (ctx->pad_texel == kTexelH16 || ctx->h_kv.wide))
+        return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "texture_filter8 is built for the u8 / fp32 texel forms below 2^24 records");
     if (ctx->timing && !ctx->events_made) {
         for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
         ctx->events_made = true;

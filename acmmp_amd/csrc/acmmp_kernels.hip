@@ -307,7 +307,10 @@ DEV float2 project(const float *H, float x, float y) {
 //          is exact in f16 (8-bit input is): 8 bytes per footprint, and the
 //          two row lerps are v_fma_mix_f32 straight from the f16 halves (the
 //          f16 -> f32 widening is exact, the fma is the pinned fp32 fma).
-constexpr int kTxWide = 1, kTxU8 = 2, kTxH16 = 4;
+//   bit 3 (kTxFrac8): acmmp_params::texture_filter8 — the bilinear fractions
+//                    rounded to the CUDA texture unit's 1.8 fixed point
+//                    (instantiated for the non-wide u8 and fp32 forms)
+constexpr int kTxWide = 1, kTxU8 = 2, kTxH16 = 4, kTxFrac8 = 8;
 
 // Source-image sampler: one buffer resource (SRD) per view over the padded
 // copy (KViews::pad), built from wave-uniform values (the view index is a
@@ -333,6 +336,7 @@ DEV SrcImage src_image(const KViews &kv, int v) {
     s.fpitch = (float)s.pitch;
     return s;
 }
+
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -456,6 +460,12 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
 }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
+// texture_filter8: a bilinear fraction in [0, 1) rounded to the texture
+// unit's 1.8 fixed point (1/256 steps, 1.0 representable), exactly: x * 256
+// and the scale back are exact, rint is round-half-even.
+DEV f2v frac8(f2v a) {
+    return f2v{__builtin_rintf(a.x * 256.0f), __builtin_rintf(a.y * 256.0f)} * 0.00390625f;
+}
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // llvm.amdgcn.struct.ptr.buffer.load: the idxen form of buffer_load
@@ -504,6 +514,7 @@ template <bool FAST, int TX>
 DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
                    RowFetch<TX> &rf) {
     constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
+    constexpr bool F8 = (TX & kTxFrac8) != 0;
     const f2v fw = splat((float)im.W), fh = splat((float)im.H);
     const f2v y = splat((float)(py - 5 + 2 * jj));
 #pragma unroll
@@ -537,6 +548,10 @@ DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v 
         const f2v fly = f2v{dm_floor(ys.x), dm_floor(ys.y)};
         rf.ax[p] = xs - flx;
         rf.ay[p] = ys - fly;
+        if (F8) {
+            rf.ax[p] = frac8(rf.ax[p]);
+            rf.ay[p] = frac8(rf.ay[p]);
+        }
         // record index (y0 + 1) * pitch + x0 + 1
         unsigned ia, ib;
         if (!WIDE) {
@@ -2045,13 +2060,16 @@ static int ns_bucket(int nsrc) {
 // index of views with 2^24 or more records; KViews::texel -> the texel form.
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
     switch ((h_kv.wide ? kTxWide : 0) | (h_kv.texel == kTexelU8 ? kTxU8 : 0) |              \
-            (h_kv.texel == kTexelH16 ? kTxH16 : 0)) {                                       \
+            (h_kv.texel == kTexelH16 ? kTxH16 : 0) | (h_kv.prm.texture_filter8 ? kTxFrac8 : 0)) { \
+        case 8: { ACMMP_LAUNCH_NSW(KERNEL, 8, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        case 10: { ACMMP_LAUNCH_NSW(KERNEL, 10, GRID, BLOCK, STREAM, __VA_ARGS__) } break;  \
         case 0: { ACMMP_LAUNCH_NSW(KERNEL, 0, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 1: { ACMMP_LAUNCH_NSW(KERNEL, 1, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 2: { ACMMP_LAUNCH_NSW(KERNEL, 2, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 3: { ACMMP_LAUNCH_NSW(KERNEL, 3, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
         case 4: { ACMMP_LAUNCH_NSW(KERNEL, 4, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        default: { ACMMP_LAUNCH_NSW(KERNEL, 5, GRID, BLOCK, STREAM, __VA_ARGS__) } break;   \
+        case 5: { ACMMP_LAUNCH_NSW(KERNEL, 5, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
+        default: return hipErrorNotSupported; /* texture_filter8 with a wide or f16 form */ \
     }
 #endif
 

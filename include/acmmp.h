@@ -75,7 +75,14 @@ typedef struct acmmp_params {
     uint32_t seed_hi;           /*   (src/ACMMP.cu:624), see include/acmmp_detmath.h */
     uint32_t rng_stream;        /* run index: a second RunPatchMatch on the same
                                    instance re-seeds like the reference's clock64() */
-    int32_t reserved[5];
+    int32_t texture_filter8;    /* 0 (default): pin A4, fp32 bilinear fractions. 1: the
+                                   CUDA texture unit's 1.8 fixed-point fractions
+                                   (cudaFilterModeLinear, src/ACMMP.cpp:659, used at
+                                   src/ACMMP.cu:394): frac rounded to 1/256 before the
+                                   lerp — an emulation (the hardware's sum order is not
+                                   documented), for fidelity studies; oracle and GPU agree
+                                   bit-exactly in both modes */
+    int32_t reserved[4];
 } acmmp_params;
 
 /* Per-kernel timing of the last run, measured with hipEvents recorded on the

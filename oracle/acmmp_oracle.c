@@ -98,8 +98,13 @@ static float tex_texel(const float *img, int W, int H, int x, int y) {
     return img[(size_t)y * W + x];
 }
 
-/* Pin P2: tex2D linear at (u+0.5, v+0.5) (src/ACMMP.cu:394). */
-static float tex_bilinear(const float *img, int W, int H, float u, float v) {
+/* texture_filter8 (acmmp_params): the CUDA texture unit's 1.8 fixed-point
+ * fraction, rounded half-even to 1/256 (x * 256 and the scale back are exact). */
+static float frac8(float a) { return rintf(a * 256.0f) * 0.00390625f; }
+
+/* Pin P2: tex2D linear at (u+0.5, v+0.5) (src/ACMMP.cu:394); q8 = the
+ * emulated 8-bit fractions of cudaFilterModeLinear instead of pin A4's fp32. */
+static float tex_bilinear(const float *img, int W, int H, float u, float v, int q8) {
     float xs = (u + 0.5f) - 0.5f;
     float ys = (v + 0.5f) - 0.5f;
     float fw = (float)W, fh = (float)H;
@@ -109,6 +114,10 @@ static float tex_bilinear(const float *img, int W, int H, float u, float v) {
     ys = (ys < fh) ? ys : fh;
     float fx0 = dm_floor(xs), fy0 = dm_floor(ys);
     float ax = xs - fx0, ay = ys - fy0;
+    if (q8) {
+        ax = frac8(ax);
+        ay = frac8(ay);
+    }
     int x0 = (int)fx0, y0 = (int)fy0;
     float t00 = tex_texel(img, W, H, x0, y0);
     float t10 = tex_texel(img, W, H, x0 + 1, y0);
@@ -418,7 +427,7 @@ static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const 
             const i2 rp = {p.x + i, p.y + j};
             const float ref_pix = tex_texel(rimg, rW, rH, rp.x, rp.y);
             f2 sp = ComputeCorrespondingPoint(H, rp);
-            const float src_pix = tex_bilinear(simg, sW, sH, sp.x, sp.y);
+            const float src_pix = tex_bilinear(simg, sW, sH, sp.x, sp.y, prm->texture_filter8);
             float w = ComputeBilateralWeight((float)i, (float)j, ref_pix, ref_center,
                                              prm->sigma_spatial, prm->sigma_color);
             const float wr = w * ref_pix;

@@ -124,6 +124,29 @@ def test_t3_photometric_cfg1_shape():
     assert np.median(rel[ok]) < 0.005
 
 
+def test_t3_texture_filter8_emulation():
+    """texture_filter8: the CUDA texture unit's 8-bit bilinear fractions
+    (cudaFilterModeLinear, src/ACMMP.cpp:659 / src/ACMMP.cu:394) instead of
+    pin A4's fp32 ones — GPU and oracle bit-exact in this mode too, and the
+    result still reconstructs the analytic depth (the mode exists to measure
+    pin A4's effect: tools/texfilter_study.py)."""
+    sc = scene.make_scene(num_views=5, width=400, height=300)
+    cams, imgs = sc.problem(2, 4)
+    prm, pl, co, sv = _gpu_run(_params(3, texture_filter8=1), cams, imgs)
+    assert prm.texture_filter8 == 1
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert_bit_exact(pl, ref["planes"], "planes")
+    assert_bit_exact(co, ref["costs"], "costs")
+    assert_bit_exact(sv, ref["selected_views"], "selected views")
+    gt = sc.views[2].depth
+    ok = (gt > 0) & (co < 0.3)
+    rel = np.abs(pl[..., 3] - gt) / np.maximum(gt, 1)
+    assert np.median(rel[ok]) < 0.005
+    # the mode changes results (it is not a no-op)
+    _, pl32, _, _ = _gpu_run(_params(3), cams, imgs)
+    assert not np.array_equal(pl32, pl)
+
+
 def test_t3_geometric_pass(small_scene):
     """Photometric pass over 4 views, then a geometric pass (Jacobi order)
     that reads their depth maps, as ProcessProblem does between passes."""

@@ -41,6 +41,10 @@ __global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, i
             case 8: case 9: case 10: case 11:                                          // k_sweep shape, 1/4 / 1/16 / 1 lane / 1/2 active
                 idx = base + r * PITCH + 2 * c + (s % 6) * 2 + (s / 6) * 2 * PITCH; break;
             case 12: h = h * 1664525u + 1013904223u; idx = (int)(h % (unsigned)nrec); break;  // random, 1/4 active
+            case 13: idx = base + (lane >> 1) + 64 * (s & 7); break;                   // lane pairs share a record
+            case 14: idx = base + (lane >> 2) + 64 * (s & 7); break;                   // lane quads share a record
+            case 15: idx = base + 3 * lane + (s & 7); break;                            // stride 3 (12 B)
+            case 16: idx = base + 8 * lane + (s & 7); break;                            // stride 8 (32 B): 4 lanes/line
             default: idx = base + lane * 33; break;                                     // one line per lane
         }
         const bool on = pattern == 8 || pattern == 12 ? (lane & 3) == 0
@@ -63,7 +67,7 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int p = 0; p < 13; ++p) {
+    for (int p = 0; p < 17; ++p) {
         for (int rep = 0; rep < 3; ++rep) {
             (void)hipEventRecord(a);
             k_gather<<<blocks, 256>>>(buf, nrec, p, out);

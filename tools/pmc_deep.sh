@@ -13,7 +13,7 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum" \
            "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU TCP_TCR_TCP_STALL_CYCLES_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $set -f csv -d gpurun_out/pmcd$i -o run -- python3 tools/quick_time.py 1600 1200 $it > gpurun_out/pmcd$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-include-regex k_sweep --pmc $set -f csv -d gpurun_out/pmcd$i -o run -- python3 tools/quick_time.py 1600 1200 $it > gpurun_out/pmcd$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
