@@ -52,6 +52,8 @@ struct acmmp_ctx {
     float4 *d_scaled = nullptr;
     size_t scaled_count = 0;
     float4 *d_seed = nullptr;
+    float *d_xsplit = nullptr;         // split sweep scratch (KState::xcost/xprob/xdesc), grow-only
+    size_t xsplit_count = 0;
     bool have_prior = false, have_scaled = false, have_seed = false, have_state = false;
 
     // Per-run constant block. A ring of pinned host / device slots so an

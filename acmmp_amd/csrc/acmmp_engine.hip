@@ -54,6 +54,8 @@ void free_state(acmmp_ctx *ctx) {
     dfree(ctx->d_mask);
     dfree(ctx->d_scaled);
     dfree(ctx->d_seed);
+    dfree(ctx->d_xsplit);
+    ctx->xsplit_count = 0;
     ctx->have_prior = ctx->have_scaled = ctx->have_seed = ctx->have_state = false;
 }
 
@@ -161,6 +163,13 @@ KState state_of(acmmp_ctx *ctx) {
     st.mask = ctx->d_mask;
     st.scaled = ctx->d_scaled;
     st.seed = ctx->d_seed;
+    st.xplane = (size_t)ctx->Wh * ctx->H;
+    if (ctx->d_xsplit) {
+        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
+        st.xcost = ctx->d_xsplit;
+        st.xprob = st.xcost + 8 * nv * st.xplane;
+        st.xdesc = reinterpret_cast<uint32_t *>(st.xprob + nv * st.xplane);
+    }
     return st;
 }
 
@@ -630,6 +639,17 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
+    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
+        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
+        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
+        if (need > ctx->xsplit_count) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
+            dfree(ctx->d_xsplit);
+            ctx->xsplit_count = 0;
+            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
+            ctx->xsplit_count = need;
+        }
+    }
     if (p.texture_filter8 && (ctx->pad_texel == kTexelH16 || ctx->h_kv.wide))
         return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "texture_filter8 is built for the u8 / fp32 texel forms below 2^24 records");
     if (ctx->timing && !ctx->events_made) {
@@ -747,6 +767,17 @@ int acmmp_eval_costs(acmmp_ctx *ctx, const float *planes4, float *out_costs, flo
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
+    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
+        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
+        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
+        if (need > ctx->xsplit_count) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
+            dfree(ctx->d_xsplit);
+            ctx->xsplit_count = 0;
+            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
+            ctx->xsplit_count = need;
+        }
+    }
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;
     float4 *d_pl = nullptr;
@@ -780,6 +811,17 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
+    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
+        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
+        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
+        if (need > ctx->xsplit_count) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
+            dfree(ctx->d_xsplit);
+            ctx->xsplit_count = 0;
+            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
+            ctx->xsplit_count = need;
+        }
+    }
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;
     float4 *d_pl = nullptr;

@@ -64,6 +64,10 @@ constexpr int kTaps = 6;
 #ifndef ACMMP_SWEEP_WAVES
 #define ACMMP_SWEEP_WAVES 2
 #endif
+// split sweep (ACMMP_SPLIT, acmmp_internal.h): waves per SIMD of its phase-A kernel
+#ifndef ACMMP_SPLIT_A_WAVES
+#define ACMMP_SPLIT_A_WAVES 3
+#endif
 
 // ----------------------------------------------------------------- textures
 DEV float texel(const float *img, int pitch, int W, int H, int x, int y) {
@@ -1159,9 +1163,15 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
 // Neighbour state is read from the colour-split "current" buffers (the
 // half-sweep snapshot); own state lives in registers and is written to the
 // "next" buffer of this colour.
-template <int NS, int TX>
-__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *__restrict__ kvp, KState st, int colour,
-                                                  int iter) {
+//   MODE 0  the whole CheckerboardPropagation (k_sweep_f)
+//   MODE 1  split sweep, A: candidate search + phase A, results to KState::xcost /
+//           xprob / xdesc (k_sweep_a: no LDS candidate slots, fewer live VGPRs,
+//           ACMMP_SPLIT_A_WAVES waves per SIMD)
+//   MODE 2  split sweep, B: view selection, current cost, refinement, accept (k_sweep_b)
+template <int NS, int TX, int MODE>
+DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int iter) {
+    static_assert(MODE == 0 || (ACMMP_CAND_LDS && ACMMP_COMPACT_REFINE && ACMMP_SELECT_REGS),
+                  "the split sweep is built on the default variants");
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
 #if ACMMP_CAND_LDS
@@ -1187,11 +1197,14 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     float my_cost = cost_same[my];
     uint32_t my_sv = st.sv[colour][my];
     if (py >= kv.sweep_rows) {  // rows the reference grid never reaches
-        st.plane_nx[colour][my] = my_plane;
-        st.cost_nx[colour][my] = my_cost;
+        if (MODE != 1) {
+            st.plane_nx[colour][my] = my_plane;
+            st.cost_nx[colour][my] = my_cost;
+        }
         return;
     }
     const acmmp_params &prm = kv.prm;
+    const size_t xp = st.xplane;  // split sweep: one plane per slot of xcost / xprob / xdesc
     const acmmp_camera &c0 = kv.cam[0];
     const int nsrc = kv.nsrc;
     const int center = py * width + px;
@@ -1201,6 +1214,13 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     // index of direction d's winner; bit d of `same`: it is this colour.
     int cidx[8];
     uint32_t flags = 0, same = 0;
+    if (MODE == 2) {  // split sweep, B: the winners phase A found (same snapshot)
+#pragma unroll
+        for (int d = 0; d < 8; ++d) cidx[d] = (int)st.xdesc[(size_t)d * xp + my];
+        const uint32_t fs = st.xdesc[(size_t)8 * xp + my];
+        flags = fs & 0xffu;
+        same = fs >> 8;
+    } else {
     float costMin;
     if (py > 2) {  // up_far (opposite colour)
         flags |= 1u << 1;
@@ -1333,14 +1353,33 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         same |= (uint32_t)bs << 6;
     }
 #undef CS
+    if (MODE == 1) {  // split sweep, A: the winners for phase B
+#pragma unroll
+        for (int d = 0; d < 8; ++d) st.xdesc[(size_t)d * xp + my] = (uint32_t)cidx[d];
+        st.xdesc[(size_t)8 * xp + my] = flags | same << 8;
+    }
+    }  // search
 #if ACMMP_CAND_LDS
     // the 8 winners' planes, fetched once into this lane's LDS slots (the
     // NCC prologues then read them at LDS latency, not L2's)
+    // (split sweep, A: no LDS slots, so more blocks fit; the planes come from
+    // L1/L2 by the same select chain as without ACMMP_CAND_LDS)
     float4 *cand_slot = cand_lds + threadIdx.y * kBX + threadIdx.x;
+    if (MODE != 1) {
 #pragma unroll
-    for (int d = 0; d < 8; ++d)
-        if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
-    auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
+        for (int d = 0; d < 8; ++d)
+            if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
+    }
+    auto cand = [&](int d) -> float4 {
+        if constexpr (MODE == 1) {
+            int ci = cidx[0];
+#pragma unroll
+            for (int e = 1; e < 8; ++e) ci = (d == e) ? cidx[e] : ci;
+            return (((same >> d) & 1u) ? plane_same : plane_opp)[ci];
+        } else {
+            return cand_slot[d * kThreads];
+        }
+    };
     auto cand_dyn = cand;
 #else
     auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
@@ -1362,10 +1401,12 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     DIAG_T(t_patch);
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
+    // (split sweep: xcost in HBM, A writes it, B reads the sampled views)
     float cost_array[8][NS];
     // view-selection inputs (:994-1032), folded into the view-major candidate
     // loop so each view's 8 costs are consumed from registers
     float probs[NS];
+    if (MODE != 2) {
     uint32_t nb[4];
     {
         const uint32_t *sv_opp = st.sv[oc];
@@ -1419,7 +1460,8 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
             float c;
             if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand_dyn(d));
             else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
-            cost_array[d][v] = c;
+            if (MODE == 1) st.xcost[(size_t)(d * nsrc + v) * xp + my] = c;
+            else cost_array[d][v] = c;
             if (c < cost_threshold) {
                 tmpw += dm_expf(c * c / (-0.18f));
                 count++;
@@ -1432,8 +1474,11 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         float pr = 0.0f;
         if (count > 2 && count_false < 3) pr = tmpw / count;
         else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
-        probs[v] = pr * vsp;
+        if (MODE == 1) st.xprob[(size_t)v * xp + my] = pr * vsp;
+        else probs[v] = pr * vsp;
     }
+    if (MODE == 1) return;  // split sweep, A ends here
+    }  // phase A
 
     DIAG_T(t_phaseA);
     // ---- multi-hypothesis joint view selection (:994-1056)
@@ -1449,7 +1494,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
         float sum = 0.0f;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            cdf[i] = i < nsrc ? probs[i] : 0.0f;
+            cdf[i] = i < nsrc ? (MODE == 2 ? st.xprob[(size_t)i * xp + my] : probs[i]) : 0.0f;
             if (i < nsrc) sum += cdf[i];
         }
         const float inv = 1.0f / sum;
@@ -1522,7 +1567,7 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
             for (int j = 0; j < NS; ++j)
                 if (j < nsrc) {
                     const float wj = (float)vw.get(j);
-                    const float cj = cost_array[i][j];
+                    const float cj = MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j];
                     fc += wj > 0 ? wj * cj : 0.0f;
                 }
             final_costs[i] = fc / weight_norm;
@@ -1538,10 +1583,11 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
             const float wj = (float)vw.get(j);
             if (wj > 0) {
                 if (prm.geom_consistency) {
-                    if (fl) fc += wj * (cost_array[i][j] + 0.2f * geom_cost(kv, j + 1, hi, px, py));
-                    else fc += wj * (cost_array[i][j] + 0.1f * 3.0f);
+                    const float cij = MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j];
+                    if (fl) fc += wj * (cij + 0.2f * geom_cost(kv, j + 1, hi, px, py));
+                    else fc += wj * (cij + 0.1f * 3.0f);
                 } else {
-                    fc += wj * cost_array[i][j];
+                    fc += wj * (MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j]);
                 }
             }
         }
@@ -1745,6 +1791,22 @@ __global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep(const KViews *
     DIAG_ADD(2, t_patch, t_phaseA);
     DIAG_ADD(3, t_phaseA, t_select);
     DIAG_ADD(4, t_select, t_end);
+}
+
+template <int NS, int TX>
+__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep_f(const KViews *__restrict__ kvp, KState st, int colour,
+                                                                    int iter) {
+    sweep_body<NS, TX, 0>(kvp, st, colour, iter);
+}
+template <int NS, int TX>
+__global__ __launch_bounds__(256, ACMMP_SPLIT_A_WAVES) void k_sweep_a(const KViews *__restrict__ kvp, KState st,
+                                                                      int colour, int iter) {
+    sweep_body<NS, TX, 1>(kvp, st, colour, iter);
+}
+template <int NS, int TX>
+__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep_b(const KViews *__restrict__ kvp, KState st, int colour,
+                                                                    int iter) {
+    sweep_body<NS, TX, 2>(kvp, st, colour, iter);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
@@ -2084,7 +2146,12 @@ hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st,
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
-    ACMMP_LAUNCH_NS(k_sweep, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+    if (kSplitSweep) {  // phase A (more waves per SIMD), then selection + refinement
+        ACMMP_LAUNCH_NS(k_sweep_a, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+        ACMMP_LAUNCH_NS(k_sweep_b, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+    } else {
+        ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+    }
     return hipGetLastError();
 }
 
