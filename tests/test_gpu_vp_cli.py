@@ -83,3 +83,17 @@ def test_world2_tcp_multi_scale_matches_oracle_jacobi(tmp_path):
     _launch(d, "/CVPMS", 2, "tcp", ["--no_fusion"], timeout=600)
     maps = OraclePipeline(d).run_multi_scale("jacobi")
     assert _compare(d + "/CVPMS", maps) == 4 * 4
+
+
+@pytest.mark.timeout(900)
+def test_world2_tcp_cfg4_source_count(tmp_path):
+    """cfg4's problem shape (each view with its 20 best sources, N = 21:
+    colmap2mvsnet_acm.py:415) through the whole schedule at world 2 — the
+    NS=32 kernel bucket inside the driver, planar prior and both geometric
+    passes — bit-exact against the oracle pipeline in Jacobi order."""
+    d = str(tmp_path / "dense_n21")
+    sc = scene.make_scene(num_views=22, width=160, height=120)
+    scene.write_dense_folder(sc, d, num_src=20)
+    _launch(d, "/CVPN21", 2, "tcp", ["--no_fusion"], timeout=600)
+    maps = OraclePipeline(d).run_single_scale("jacobi")
+    assert _compare(d + "/CVPN21", maps) == 22 * 4
