@@ -32,6 +32,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -114,7 +115,15 @@ class Group {
             if (::bind(ls, (sockaddr *)&a, sizeof a) || ::listen(ls, world))
                 fail("rendezvous: cannot listen on port " + std::to_string(port));
             peers_.assign(world, -1);
+            const char *to = std::getenv("ACMMP_RDZV_TIMEOUT");  // seconds for every rank to arrive
+            const int timeout_ms = 1000 * (to && *to ? std::atoi(to) : 600);
             for (int k = 1; k < world; ++k) {
+                pollfd pf{ls, POLLIN, 0};
+                if (::poll(&pf, 1, timeout_ms) != 1) {
+                    ::close(ls);
+                    fail("rendezvous: " + std::to_string(world - k) + " rank(s) did not connect to port " +
+                         std::to_string(port) + " in time");
+                }
                 const int fd = ::accept(ls, nullptr, nullptr);
                 if (fd < 0) fail("rendezvous accept failed");
                 ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
