@@ -16,6 +16,19 @@
 
 using namespace acmmp;
 
+// acmmp_texture_create: one view's padded footprint records (KViews::pad),
+// built once and borrowed by any engine on the device (~ a CUDA texture
+// object, src/ACMMP.cpp:640-662). The image itself stays the caller's.
+struct acmmp_texture {
+    int device = 0;
+    const float *img = nullptr;  // borrowed, row pitch img_pitch floats
+    int img_pitch = 0;
+    int W = 0, H = 0;
+    int form = 0;                // kTexelF32 / kTexelU8 / kTexelH16
+    float *pad = nullptr;        // owned
+    int pad_pitch = 0;           // records per row
+};
+
 struct acmmp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -32,6 +45,7 @@ struct acmmp_ctx {
     std::vector<const float *> img, dep;
     std::vector<int> img_pitch;
     std::vector<float *> pad;          // padded source images (KViews::pad), owned
+    std::vector<const float *> pad_use;  // what KViews::pad points at: pad[i] or a texture's records
     std::vector<size_t> pad_bytes;
     std::vector<int> pad_pitch;
     int pad_texel = 0;                 // form of pad[] (KViews::texel, kTexel*)

@@ -97,7 +97,7 @@ int kv_upload(acmmp_ctx *ctx) {
         kv.cam[i] = ctx->cams[i];
         kv.img[i] = ctx->img[i];
         kv.ipitch[i] = ctx->img_pitch[i];
-        kv.pad[i] = ctx->pad[i];
+        kv.pad[i] = ctx->pad_use[i];
         kv.ppitch[i] = ctx->pad_pitch[i];
         if (i > 0) kv.rel[i] = view_rel(ctx->cams[0], ctx->cams[i]);
         if (ctx->have_depths) {
@@ -215,9 +215,44 @@ int set_depths_impl(acmmp_ctx *ctx, const float *const *depths, const int32_t *p
     return ACMMP_OK;
 }
 
+// Records per row and bytes of one view's padded footprint records in
+// `form` (128-B rows: u8 quads W + 2, f16 quads W + 2, fp32 row pairs
+// W + 3; sized for the fp32 form, the largest). Non-zero: too large.
+int pad_geometry(int w, int h, int form, int &pp, size_t &bytes) {
+    const int pf = (w + 3 + 15) / 16 * 16;
+    pp = form == kTexelU8 ? (w + 2 + 31) / 32 * 32 : form == kTexelH16 ? (w + 2 + 15) / 16 * 16 : pf;
+    bytes = (size_t)pf * (h + 2) * 2 * sizeof(float);
+    // the gather kernels index records with a 24x24-bit multiply into a
+    // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
+    return ((size_t)pf * (h + 2) >= (1u << 31) || pf >= (1 << 24) || h + 2 >= (1 << 24)) ? 1 : 0;
+}
+
+hipError_t launch_pad_form(int form, const float *img, int pitch, int w, int h, float *pad, int pp,
+                           uint32_t *d_unfit, hipStream_t s) {
+    if (form == kTexelF32) return launch_pad_image(img, pitch, w, h, pad, pp, s);
+    if (form == kTexelU8) return launch_pad_quad(img, pitch, w, h, reinterpret_cast<uint32_t *>(pad), pp, d_unfit, s);
+    return launch_pad_h16(img, pitch, w, h, pad, pp, d_unfit, s);
+}
+
+// The compact forms to try before fp32, as ACMMP_TEXEL / ACMMP_TEXEL_F32 restrict them.
+int texel_tries(int tries[2]) {
+    tries[0] = kTexelU8;
+    tries[1] = kTexelH16;
+    int ntry = 2;
+    if (const char *e = std::getenv("ACMMP_TEXEL")) {
+        if (!std::strcmp(e, "f32")) ntry = 0;
+        else if (!std::strcmp(e, "u8")) ntry = 1;
+        else if (!std::strcmp(e, "h16")) { tries[0] = kTexelH16; ntry = 1; }
+    }
+    if (const char *e = std::getenv("ACMMP_TEXEL_F32"))
+        if (e[0] == '1') ntry = 0;
+    return ntry;
+}
+
 // Shared by acmmp_set_images / acmmp_set_images_device.
 int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, const float *const *images,
-                    const int32_t *pitches, int keep_depth_range, bool borrow) {
+                    const int32_t *pitches, int keep_depth_range, bool borrow,
+                    const acmmp_texture *const *tex = nullptr) {
     if (!ctx) return ACMMP_ERR_ARG;
     if (num_images < 2 || num_images > ACMMP_MAX_IMAGES)
         return set_err(ctx, ACMMP_ERR_ARG, "num_images=%d outside [2, %d]", num_images, ACMMP_MAX_IMAGES);
@@ -270,21 +305,23 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         ctx->pad.resize(num_images, nullptr);
         ctx->pad_bytes.resize(num_images, 0);
         ctx->pad_pitch.resize(num_images, 0);
+        ctx->pad_use.resize(num_images, nullptr);
     }
+    if (tex) {  // prebuilt records of one common form: borrowed, nothing to pad
+        for (int i = 0; i < num_images; ++i) {
+            ctx->pad_use[i] = tex[i]->pad;
+            ctx->pad_pitch[i] = tex[i]->pad_pitch;
+        }
+        ctx->pad_texel = tex[0]->form;
+    } else {
     // The most compact form every view fits, each attempt checked by one
     // device flag (one stream sync): u8 quads (4 B per footprint: every view
     // integer-valued in [0, 255]), then f16 difference quads (8 B: every
     // stored value exact in f16), else the fp32 row-paired form (16 B).
     // ACMMP_TEXEL=u8|h16|f32 restricts the attempt to that one form before
     // fp32 (ACMMP_TEXEL_F32=1 = f32): the parity tests of every form.
-    int tries[2] = {kTexelU8, kTexelH16}, ntry = 2;
-    if (const char *e = std::getenv("ACMMP_TEXEL")) {
-        if (!std::strcmp(e, "f32")) ntry = 0;
-        else if (!std::strcmp(e, "u8")) ntry = 1;
-        else if (!std::strcmp(e, "h16")) { tries[0] = kTexelH16; ntry = 1; }
-    }
-    if (const char *e = std::getenv("ACMMP_TEXEL_F32"))
-        if (e[0] == '1') ntry = 0;
+    int tries[2];
+    const int ntry = texel_tries(tries);
     if (!ctx->d_not_u8) HIP_TRY(ctx, dalloc(ctx->d_not_u8, 1));
     ctx->pad_texel = -1;
     for (int k = 0; k <= ntry && ctx->pad_texel < 0; ++k) {
@@ -292,14 +329,9 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         if (form != kTexelF32) HIP_TRY(ctx, hipMemsetAsync(ctx->d_not_u8, 0, sizeof(uint32_t), ctx->stream));
         for (int i = 0; i < num_images; ++i) {
             const int w = cams[i].width, h = cams[i].height;
-            // records per row (128-B rows): u8 quads W + 2, f16 quads W + 2,
-            // fp32 row pairs W + 3; the f32 form is the largest allocation
-            const int pf = (w + 3 + 15) / 16 * 16;
-            const int pp = form == kTexelU8 ? (w + 2 + 31) / 32 * 32 : form == kTexelH16 ? (w + 2 + 15) / 16 * 16 : pf;
-            const size_t bytes = (size_t)pf * (h + 2) * 2 * sizeof(float);
-            // the gather kernels index records with a 24x24-bit multiply into a
-            // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
-            if ((size_t)pf * (h + 2) >= (1u << 31) || pf >= (1 << 24) || h + 2 >= (1 << 24))
+            int pp;
+            size_t bytes;
+            if (pad_geometry(w, h, form, pp, bytes))
                 return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "view %d is %dx%d: above the 2^31-record gather limit", i,
                                w, h);
             if (ctx->pad_bytes[i] < bytes) {
@@ -308,15 +340,9 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
                 ctx->pad_bytes[i] = bytes;
             }
             ctx->pad_pitch[i] = pp;
-            if (form == kTexelF32)
-                HIP_TRY(ctx, launch_pad_image(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->stream));
-            else if (form == kTexelU8)
-                HIP_TRY(ctx, launch_pad_quad(ctx->img[i], ctx->img_pitch[i], w, h,
-                                             reinterpret_cast<uint32_t *>(ctx->pad[i]), pp, ctx->d_not_u8,
-                                             ctx->stream));
-            else
-                HIP_TRY(ctx, launch_pad_h16(ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->d_not_u8,
-                                            ctx->stream));
+            ctx->pad_use[i] = ctx->pad[i];
+            HIP_TRY(ctx, launch_pad_form(form, ctx->img[i], ctx->img_pitch[i], w, h, ctx->pad[i], pp, ctx->d_not_u8,
+                                         ctx->stream));
         }
         if (form == kTexelF32) {
             ctx->pad_texel = kTexelF32;
@@ -327,6 +353,7 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
             if (unfit == 0) ctx->pad_texel = form;
         }
     }
+    }  // padded copies
     if (resize || !ctx->d_rm_plane) {
         free_state(ctx);
         const size_t P = (size_t)ctx->W * ctx->H;
@@ -488,6 +515,96 @@ int acmmp_set_images(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, c
 int acmmp_set_images_device(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
                             const float *const *d_images, const int32_t *pitches, int keep_depth_range) {
     return set_images_impl(ctx, num_images, cams, d_images, pitches, keep_depth_range, true);
+}
+
+int acmmp_texture_create(int device, const float *d_image, int pitch, int width, int height, acmmp_texture **out) {
+    if (!out || !d_image || width < 2 || height < 1 || pitch < width) return ACMMP_ERR_ARG;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    auto *t = new (std::nothrow) acmmp_texture;
+    if (!t) return ACMMP_ERR_HIP;
+    t->device = device;
+    t->img = d_image;
+    t->img_pitch = pitch;
+    t->W = width;
+    t->H = height;
+    hipStream_t s = nullptr;
+    uint32_t *d_unfit = nullptr;
+    int rc = ACMMP_OK;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&d_unfit, sizeof(uint32_t)) != hipSuccess)
+        rc = ACMMP_ERR_HIP;
+    // the most compact form the image fits (the choice set_images makes per problem)
+    int tries[2];
+    const int ntry = texel_tries(tries);
+    t->form = -1;
+    for (int k = 0; rc == ACMMP_OK && k <= ntry && t->form < 0; ++k) {
+        const int form = k < ntry ? tries[k] : kTexelF32;
+        size_t bytes;
+        if (pad_geometry(width, height, form, t->pad_pitch, bytes)) {
+            rc = ACMMP_ERR_UNSUPPORTED;
+            break;
+        }
+        if (!t->pad && hipMalloc((void **)&t->pad, bytes) != hipSuccess) {
+            rc = ACMMP_ERR_HIP;
+            break;
+        }
+        uint32_t unfit = 0;
+        if (hipMemsetAsync(d_unfit, 0, sizeof(uint32_t), s) != hipSuccess ||
+            launch_pad_form(form, d_image, pitch, width, height, t->pad, t->pad_pitch, d_unfit, s) != hipSuccess ||
+            hipMemcpyAsync(&unfit, d_unfit, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            rc = ACMMP_ERR_HIP;
+            break;
+        }
+        if (form == kTexelF32 || unfit == 0) t->form = form;
+    }
+    if (d_unfit) (void)hipFree(d_unfit);
+    if (s) (void)hipStreamDestroy(s);
+    if (rc != ACMMP_OK) {
+        acmmp_texture_destroy(t);
+        return rc;
+    }
+    *out = t;
+    return ACMMP_OK;
+}
+
+void acmmp_texture_destroy(acmmp_texture *t) {
+    if (!t) return;
+    if (t->pad) {
+        (void)hipSetDevice(t->device);
+        (void)hipFree(t->pad);
+    }
+    delete t;
+}
+
+int acmmp_texture_bits(const acmmp_texture *t) {
+    if (!t) return 0;
+    return t->form == kTexelU8 ? 8 : t->form == kTexelH16 ? 16 : 32;
+}
+
+int acmmp_set_images_textures(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
+                              const acmmp_texture *const *textures, int keep_depth_range) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    if (!cams || !textures || num_images < 2 || num_images > ACMMP_MAX_IMAGES)
+        return set_err(ctx, ACMMP_ERR_ARG, "bad textures");
+    const float *imgs[ACMMP_MAX_IMAGES];
+    int32_t pitches[ACMMP_MAX_IMAGES];
+    bool common = true;
+    for (int i = 0; i < num_images; ++i) {
+        const acmmp_texture *t = textures[i];
+        if (!t) return set_err(ctx, ACMMP_ERR_ARG, "texture %d is NULL", i);
+        if (t->device != ctx->device) return set_err(ctx, ACMMP_ERR_ARG, "texture %d is on device %d", i, t->device);
+        if (t->W != cams[i].width || t->H != cams[i].height)
+            return set_err(ctx, ACMMP_ERR_ARG, "texture %d is %dx%d, camera %dx%d", i, t->W, t->H, cams[i].width,
+                           cams[i].height);
+        imgs[i] = t->img;
+        pitches[i] = t->img_pitch;
+        common = common && t->form == textures[0]->form;
+    }
+    // views of different forms (one not 8-bit, say): pad per engine in the common form
+    return set_images_impl(ctx, num_images, cams, imgs, pitches, keep_depth_range, true,
+                           common ? textures : nullptr);
 }
 
 int acmmp_set_depth_maps(acmmp_ctx *ctx, const float *const *depths) {

@@ -334,6 +334,7 @@ class Driver {
         for (auto &t : writers_)
             if (t.joinable()) t.join();
         for (auto *e : engines_) acmmp_destroy(e);
+        for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
     }
 
     void run() {
@@ -419,6 +420,8 @@ class Driver {
     }
 
     void load_views() {
+        for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
+        textures_.clear();
         images_.clear();
         cams_.clear();
         host_images_.clear();
@@ -459,10 +462,17 @@ class Driver {
         for (auto &t : pool) t.join();
         for (size_t k = 0; k < need.size(); ++k)
             if (!errs[k].empty()) fail("view " + std::to_string(need[k]) + ": " + errs[k]);
+        for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
+        textures_.clear();
         for (size_t k = 0; k < need.size(); ++k) {
             DevBuf d(host[k].size());
             hip_check(hipMemcpy(d.p, host[k].data(), host[k].size() * sizeof(float), hipMemcpyHostToDevice),
                       "hipMemcpy");
+            // the padded footprint records, built once per image and scale
+            acmmp_texture *t = nullptr;
+            acmmp_check(acmmp_texture_create(o_.device, d.p, cams[k].width, cams[k].width, cams[k].height, &t),
+                        "acmmp_texture_create");
+            textures_[need[k]] = t;
             images_.emplace(need[k], std::move(d));
             cams_[need[k]] = cams[k];
             host_images_[need[k]] = std::move(host[k]);
@@ -528,15 +538,15 @@ class Driver {
         std::vector<int> ids = {pr.ref_image_id};
         for (int s = 0; s < pr.num_src_images; ++s) ids.push_back(pr.src_image_ids[s]);
         std::vector<acmmp_camera> cams;
-        std::vector<const float *> imgs;
+        std::vector<const acmmp_texture *> tex;
         for (int id : ids) {
             cams.push_back(cams_.at(id));
-            imgs.push_back(images_.at(id).p);
+            tex.push_back(textures_.at(id));
         }
         const acmmp_params p = view_params(t);
         acmmp_check(acmmp_set_params(eng, &p), "acmmp_set_params", eng);
-        acmmp_check(acmmp_set_images_device(eng, (int)ids.size(), cams.data(), imgs.data(), nullptr, 0),
-                    "acmmp_set_images_device", eng);
+        acmmp_check(acmmp_set_images_textures(eng, (int)ids.size(), cams.data(), tex.data(), 0),
+                    "acmmp_set_images_textures", eng);
         const int W = cams[0].width, H = cams[0].height;
         ViewState &prev = state_[t.v];
         if (t.geom) {
@@ -689,6 +699,7 @@ class Driver {
     std::vector<int> mine_;
     std::vector<acmmp_ctx *> engines_;
     std::map<int, DevBuf> images_;
+    std::map<int, acmmp_texture *> textures_;  // ~ the reference's texture objects, per image and scale
     std::map<int, acmmp_camera> cams_;
     std::map<int, std::vector<float>> host_images_;
     std::vector<std::pair<int, int>> shape_;

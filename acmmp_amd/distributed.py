@@ -110,6 +110,7 @@ class ViewTask:
     depths: Optional[list] = None          # source depth maps (tensor views, any row pitch), geom passes
     state: Optional[tuple] = None          # (planes (H,W,4), costs (H,W)) tensors, geom passes
     hier_inputs: Optional[tuple] = None    # (scaled planes (sh,sw,4), upsampled depth (H,W)) tensors
+    textures: Optional[list] = None        # engine.Texture per image (prebuilt footprint records)
 
 
 @dataclass
@@ -148,7 +149,10 @@ def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
     planes = torch.empty((H, W, 4), dtype=torch.float32, device=ref.device)
     costs = torch.empty((H, W), dtype=torch.float32, device=ref.device)
     eng.set_params(_view_params(t))
-    eng.set_images_device(t.cams, [im.data_ptr() for im in t.images], [im.stride(0) for im in t.images])
+    if t.textures is not None:
+        eng.set_images_textures(t.cams, t.textures)
+    else:
+        eng.set_images_device(t.cams, [im.data_ptr() for im in t.images], [im.stride(0) for im in t.images])
     if t.geom:
         eng.set_depth_maps_device([d.data_ptr() for d in t.depths], [d.stride(0) for d in t.depths])
         eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
@@ -294,6 +298,12 @@ class ViewParallelPipeline:
             self.images[i] = torch.from_numpy(img).to(self.tdev)
             self.cams[i] = cam
         self._sync()
+        # one texture (padded footprint records) per image and scale, shared by
+        # every view and pass of the scale (engine runs only)
+        self.textures = {}
+        if self.compute is engine_compute and self.tdev.type == "cuda":
+            from .engine import Texture
+            self.textures = {i: Texture.of(im, self.device) for i, im in self.images.items()}
 
     @contextmanager
     def _timed(self, name: str):
@@ -337,7 +347,9 @@ class ViewParallelPipeline:
             p = self.problems[v]
             ids = [p.ref_image_id] + p.sources
             t = ViewTask(index=v, ref_id=p.ref_image_id, ids=ids, cams=[self.cams[i] for i in ids],
-                         images=[self.images[i] for i in ids], geom=geom, planar=planar, hierarchy=hierarchy,
+                         images=[self.images[i] for i in ids],
+                         textures=[self.textures[i] for i in ids] if self.textures else None,
+                         geom=geom, planar=planar, hierarchy=hierarchy,
                          multi=multi, seed_lo=self.seed + p.ref_image_id, seed_hi=self.pass_index,
                          max_iterations=self.max_iterations)
             if geom:

@@ -94,6 +94,44 @@ def joint_bilateral_upsample_device(d_image: int, width: int, height: int, d_dep
     return isc.value
 
 
+class Texture:
+    """~ a CUDA texture object (src/ACMMP.cpp:640-662): the padded footprint
+    records of one device-resident image, built once and borrowed by every
+    engine/run that uses the image (acmmp_texture_create). Keep the image
+    tensor alive while the texture is used."""
+
+    def __init__(self, d_image: int, width: int, height: int, pitch: int | None = None, device: int = 0):
+        self._lib = _abi.load_library()
+        h = C.c_void_p()
+        rc = self._lib.acmmp_texture_create(int(device), C.c_void_p(int(d_image)), int(pitch or width), int(width),
+                                            int(height), C.byref(h))
+        if rc != 0:
+            raise AcmmpError(f"acmmp_texture_create failed (status {rc})")
+        self._h = h
+        self.width, self.height = int(width), int(height)
+
+    @classmethod
+    def of(cls, image, device: int = 0) -> "Texture":
+        """From an (H, W) float32 device tensor."""
+        return cls(image.data_ptr(), image.shape[1], image.shape[0], image.stride(0), device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def bits(self) -> int:
+        return int(self._lib.acmmp_texture_bits(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.acmmp_texture_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 def device_count() -> int:
     return int(_abi.load_library().acmmp_device_count())
 
@@ -207,6 +245,15 @@ class ACMMP:
         pit = None if pitches is None else (C.c_int32 * n)(*pitches)
         self._check(self._lib.acmmp_set_images_device(self._ctx, n, cam_arr, arr, pit, int(keep_depth_range)),
                     "acmmp_set_images_device")
+
+    def set_images_textures(self, cams: Sequence[_abi.Camera], textures: Sequence["Texture"],
+                            keep_depth_range: bool = False):
+        """set_images_device from prebuilt textures (no per-run padding)."""
+        n = len(cams)
+        cam_arr = (_abi.Camera * n)(*cams)
+        arr = (C.c_void_p * n)(*[t.handle for t in textures])
+        self._check(self._lib.acmmp_set_images_textures(self._ctx, n, cam_arr, arr, int(keep_depth_range)),
+                    "acmmp_set_images_textures")
 
     def set_plane_hypotheses_device(self, d_planes: int, d_costs: int):
         self._check(self._lib.acmmp_set_plane_hypotheses_device(self._ctx, C.c_void_p(int(d_planes)),

@@ -105,14 +105,22 @@ class EnginePool:
         return results
 
 
+def _set_images(eng: ACMMP, cams, image_ptrs, pitches, textures):
+    if textures is not None:  # prebuilt footprint records: no per-run padding
+        eng.set_images_textures(cams, textures)
+    else:
+        eng.set_images_device(cams, image_ptrs, pitches)
+
+
 def photometric_view(pool: EnginePool, eng: ACMMP, params: _abi.Params, cams: Sequence[_abi.Camera],
                      image_ptrs: Sequence[int], planes_out: int, costs_out: int, depth_out: int = 0,
-                     pitches: Optional[Sequence[int]] = None) -> _abi.Params:
+                     pitches: Optional[Sequence[int]] = None, textures: Optional[Sequence] = None) -> _abi.Params:
     """Photometric RunPatchMatch of one view; results exported to device
     buffers (planes (H,W,4), costs (H,W), depth (H,W) = planes[..., 3]).
-    Returns the parameters the run used (for the oracle)."""
+    Images come from `textures` (engine.Texture, one per view) when given,
+    else borrowed from `image_ptrs`. Returns the parameters the run used."""
     eng.set_params(params)
-    eng.set_images_device(cams, image_ptrs, pitches)
+    _set_images(eng, cams, image_ptrs, pitches, textures)
     used = eng.params
     eng.run_async()
     eng.export_results(planes_out, costs_out, depth_out)
@@ -124,13 +132,13 @@ def geometric_view(pool: EnginePool, eng: ACMMP, params: _abi.Params, cams: Sequ
                    image_ptrs: Sequence[int], depth_ptrs: Sequence[int], planes: int, costs: int,
                    planes_out: int = 0, costs_out: int = 0, depth_out: int = 0,
                    pitches: Optional[Sequence[int]] = None,
-                   depth_pitches: Optional[Sequence[int]] = None) -> _abi.Params:
+                   depth_pitches: Optional[Sequence[int]] = None, textures: Optional[Sequence] = None) -> _abi.Params:
     """Geometric-consistency RunPatchMatch of one view from the previous
     pass's state (planes/costs, device) and the source depth maps (device,
     e.g. slices of an all-gather). `params` must carry geom_consistency and
     the pass's max_iterations. Outputs default to overwriting the inputs."""
     eng.set_params(params)
-    eng.set_images_device(cams, image_ptrs, pitches)
+    _set_images(eng, cams, image_ptrs, pitches, textures)
     eng.set_depth_maps_device(depth_ptrs, depth_pitches)
     eng.set_plane_hypotheses_device(planes, costs)
     used = eng.params
@@ -153,8 +161,11 @@ class ResidentViews:
     def __init__(self, pool: EnginePool, cams: dict, images: dict, sources: dict, mine: Sequence[int],
                  height: int, width: int, total_views: Optional[int] = None, base_id: int = 0):
         import torch
+        from .engine import Texture
         self.pool = pool
         self.cams, self.images, self.sources = cams, images, sources
+        # one texture per image, shared by every view, engine and pass
+        self.textures = {i: Texture.of(im, pool.device) for i, im in images.items()}
         self.mine = list(mine)
         self.base_id = base_id
         dev = next(iter(images.values())).device
@@ -179,7 +190,8 @@ class ResidentViews:
             ids = self._ids(v)
             self.used_params[("photo", v)] = photometric_view(
                 self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
-                self.planes[k].data_ptr(), self.costs[k].data_ptr(), self.my_depth[k].data_ptr())
+                self.planes[k].data_ptr(), self.costs[k].data_ptr(), self.my_depth[k].data_ptr(),
+                textures=[self.textures[i] for i in ids])
         self.pool.map(one, list(enumerate(self.mine)))
 
     def geometric_pass(self, params: _abi.Params):
@@ -192,5 +204,5 @@ class ResidentViews:
             self.used_params[("geom", v)] = geometric_view(
                 self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
                 [self.all_depth[self._depth_index(i)].data_ptr() for i in ids],
-                self.planes[k].data_ptr(), self.costs[k].data_ptr())
+                self.planes[k].data_ptr(), self.costs[k].data_ptr(), textures=[self.textures[i] for i in ids])
         self.pool.map(one, list(enumerate(self.mine)))

@@ -174,6 +174,24 @@ int acmmp_set_images_device(acmmp_ctx *ctx, int num_images, const acmmp_camera *
                             const float *const *d_images, const int32_t *pitches,
                             int keep_depth_range);
 
+/* ~ cudaCreateTextureObject of one view (src/ACMMP.cpp:640-662): the padded
+ * bilinear-footprint records of a device-resident grayscale image (row pitch
+ * in floats), in the most compact form it fits, built once on `device` and
+ * borrowed by every engine and run that uses the image, so no run re-pads it.
+ * The image stays the caller's and must outlive the texture's use. */
+typedef struct acmmp_texture acmmp_texture;
+int acmmp_texture_create(int device, const float *d_image, int pitch, int width, int height,
+                         acmmp_texture **out);
+/* ~ cudaDestroyTextureObject (src/ACMMP.cpp:122-128). NULL is a no-op. */
+void acmmp_texture_destroy(acmmp_texture *tex);
+/* Bits per texel of the records: 8 (u8 quads), 16 (f16) or 32 (fp32). */
+int acmmp_texture_bits(const acmmp_texture *tex);
+/* acmmp_set_images_device from textures (index 0 = reference view): the
+ * engine borrows their images and records. Textures of different forms are
+ * re-padded per engine in their common form, as acmmp_set_images_device does. */
+int acmmp_set_images_textures(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams,
+                              const acmmp_texture *const *textures, int keep_depth_range);
+
 /* Previous-pass state for the reuse init branch (src/ACMMP.cpp:718-742):
  * planes = (world-frame normal xyz, depth) float4 per ref pixel, costs per pixel. */
 int acmmp_set_plane_hypotheses(acmmp_ctx *ctx, const float *planes4, const float *costs);

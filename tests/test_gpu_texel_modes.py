@@ -114,3 +114,30 @@ def test_quads_at_image_borders(monkeypatch, form, bits):
     got, prm, pl, co, sv = _run(cams, imgs, iters=3)
     assert got == bits
     _check(prm, cams, imgs, pl, co, sv, f"{form} borders")
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_textures_match_oracle(prob, mixed):
+    """acmmp_texture_create + acmmp_set_images_textures (records built once,
+    borrowed by the engine: the drivers' and bench's path). mixed: one view
+    holds fractional texels, so its texture is fp32 while the others are u8
+    quads; the engine then re-pads the problem in the common (fp32) form."""
+    import torch
+    from acmmp_amd.engine import Texture
+    cams, imgs = prob
+    imgs = [np.asarray(im, np.float32).copy() for im in imgs]
+    if mixed:
+        imgs[3] = imgs[3] + 0.1  # not exact in f16 either: the fp32 form
+    dev = torch.device("cuda", 0)
+    timgs = [torch.from_numpy(im).to(dev) for im in imgs]
+    torch.cuda.synchronize()
+    tex = [Texture.of(t, 0) for t in timgs]
+    assert [t.bits for t in tex] == [32 if (mixed and i == 3) else 8 for i in range(len(tex))]
+    with ACMMP(0) as eng:
+        eng.set_params(_params(2))
+        eng.set_images_textures(cams, tex)
+        assert eng.texel_bits() == (32 if mixed else 8)
+        prm = eng.params
+        eng.RunPatchMatch()
+        pl, co, sv = eng.plane_hypotheses(), eng.costs(), eng.selected_views()
+    _check(prm, cams, imgs, pl, co, sv, "textures, mixed" if mixed else "textures")
