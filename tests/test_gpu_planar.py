@@ -96,3 +96,43 @@ def test_planar_pass_end_to_end(first_pass):
     assert_bit_exact(second[0], ref1["planes"], "planar pass planes")
     assert_bit_exact(second[1], ref1["costs"], "planar pass costs")
     assert_bit_exact(second[2], ref1["selected_views"], "planar pass selected views")
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_full_size_planar_pass():
+    """cfg3 (BASELINE configs[2]) at its full size: one 1600x1200 reference
+    view with 9 sources, 8 iterations — photometric run, planar prior built
+    on the device (support points, Delaunay, raster, plane fit, range check),
+    planar-prior run — bit-exact against the oracle at every stage."""
+    import torch
+    dev = torch.device("cuda", 0)
+    setup = scene.scene_setup(num_views=10, width=1600, height=1200)
+    ids = [0] + setup.pairs[0][:9]
+    timgs = [scene.render_torch(setup, i, dev) for i in ids]
+    imgs = [t.cpu().numpy() for t in timgs]
+    cams = [setup.camera(i) for i in ids]
+    p = default_params()
+    p.max_iterations = 8
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        prm0 = eng.params
+        eng.RunPatchMatch()
+        first_planes, first_costs = eng.plane_hypotheses(), eng.costs()
+        pts = eng.GetSupportPoints()
+        tris = eng.DelaunayTriangulation(pts)
+        npts, ntri = eng.prepare_planar_prior()
+        assert (npts, ntri) == (pts.shape[0], tris.shape[0]) and ntri > 10000
+        prm1 = eng.params
+        eng.RunPatchMatch()
+        second = (eng.plane_hypotheses(), eng.costs(), eng.selected_views())
+    ref0 = oracle.run_patchmatch(prm0, cams, imgs)
+    assert_bit_exact(first_planes, ref0["planes"], "cfg3 photometric planes")
+    assert_bit_exact(first_costs, ref0["costs"], "cfg3 photometric costs")
+    np.testing.assert_array_equal(pts, oracle.support_points(ref0["costs"]))
+    _, mask, prior = oracle.planar_prior(cams[0], ref0["planes"][..., 3], prm1.depth_min, prm1.depth_max, tris)
+    ref1 = oracle.run_patchmatch(prm1, cams, imgs, planes=ref0["planes"], costs=ref0["costs"],
+                                 prior_planes=prior, masks=mask)
+    assert_bit_exact(second[0], ref1["planes"], "cfg3 planar pass planes")
+    assert_bit_exact(second[1], ref1["costs"], "cfg3 planar pass costs")
+    assert_bit_exact(second[2], ref1["selected_views"], "cfg3 planar pass selected views")
