@@ -442,7 +442,7 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             const float r = tile[tb + ii + 2 * kTileW * jj];
             const float w = bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
             const float wr = w * r;
-            r_ref += wr;
+            r_ref = dm_fma(w, r, r_ref);  // nvcc's contraction of `sum += w * r` (pin P3)
             r_rr = dm_fma(wr, r, r_rr);
             r_w += w;
             float *slot = reinterpret_cast<float *>(&pp.w[wslot(ii >> 1, jj) * kThreads]);
@@ -457,9 +457,8 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
     }
     const float inv = 1.0f / bw;
     sum_ref *= inv;
-    sum_rr *= inv;
     pp.mean = sum_ref;
-    pp.var = sum_rr - sum_ref * sum_ref;
+    pp.var = dm_fma(sum_rr, inv, -(sum_ref * sum_ref));  // `rr * inv - m * m` contracted (pin P3)
     pp.inv_wsum = inv;
 }
 
@@ -637,7 +636,7 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
         const f2v wr = wv * f2v{rr[0], rr[1]};
 #endif
         const f2v ws = wv * sv;
-        acc_s[p] += ws;
+        acc_s[p] = fma2(wv, sv, acc_s[p]);  // `sum += w * s` contracted (pin P3)
         acc_ss[p] = fma2(ws, sv, acc_ss[p]);
         acc_rs[p] = fma2(wr, sv, acc_rs[p]);
     }
@@ -755,11 +754,9 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #endif
     sum_src *= pp.inv_wsum;
-    sum_ss *= pp.inv_wsum;
-    sum_rs *= pp.inv_wsum;
-    const float var_src = sum_ss - sum_src * sum_src;
+    const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
     if (var_src < kMinVar) return cost_max;
-    const float covar = sum_rs - pp.mean * sum_src;
+    const float covar = dm_fma(sum_rs, pp.inv_wsum, -(pp.mean * sum_src));
     const float var_rs = dm_sqrt(pp.var * var_src);
     float c = 1.0f - covar / var_rs;
     c = (c < cost_max) ? c : cost_max;
@@ -2146,7 +2143,7 @@ hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st,
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
-    if (kSplitSweep) {  // phase A (more waves per SIMD), then selection + refinement
+    if constexpr (kSplitSweep) {  // phase A (more waves per SIMD), then selection + refinement
         ACMMP_LAUNCH_NS(k_sweep_a, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
         ACMMP_LAUNCH_NS(k_sweep_b, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
     } else {

@@ -194,4 +194,14 @@ DM_FN float dm_rng_uniform(dm_rng *g) {
     return dm_uniform(x);
 }
 
+
+/* Fidelity-study builds only (-DACMMP_CUDA_NUMERICS, tools/fidelity_study.py):
+ * device code takes the reference's --use_fast_math intrinsics
+ * (src/CMakeLists.txt:19) instead of the pinned functions. Such a build is
+ * NOT bit-exact with the oracle and never ships. */
+#if defined(ACMMP_CUDA_NUMERICS) && defined(__HIP_DEVICE_COMPILE__)
+#define dm_expf(x) __expf(x)
+#define dm_sinf(x) __sinf(x)
+#define dm_cosf(x) __cosf(x)
+#endif
 #endif /* ACMMP_DETMATH_H_ */

@@ -34,9 +34,14 @@
  *      x0=floor, a=xs-x0, texels clamp-to-edge, lerp = fma(a, t1-t0, t0).
  *   P4 ComputeHomography (src/ACMMP.cu:292-311): x/w, x/K[0], x/K[4] are
  *      x*(1/w), x*(1/K[0]), x*(1/K[4]) with the reciprocal exactly rounded.
- *   P3 NCC sums (src/ACMMP.cu:382-412), per sample: ws=w*s; row_s+=ws;
- *      row_ss=fma(ws,s,row_ss); row_rs=fma(w*r,s,row_rs); ref side likewise
- *      (wr=w*r; row_r+=wr; row_rr=fma(wr,r,row_rr); row_w+=w).
+ *   P3 NCC sums and moments (src/ACMMP.cu:382-430) as nvcc's default
+ *      contraction (--fmad=true, implied by the reference's --use_fast_math,
+ *      src/CMakeLists.txt:19) forms them: per sample row_s=fma(w,s,row_s),
+ *      row_ss=fma(w*s,s,row_ss), row_rs=fma(w*r,s,row_rs), ref side likewise
+ *      (row_r=fma(w,r,row_r); row_rr=fma(w*r,r,row_rr); row_w+=w); then
+ *      with m=sum*inv, var=fma(sum_xx,inv,-(m*m)), covar=fma(sum_rs,inv,
+ *      -(m_r*m_s)) (LLVM's fsub combine fuses the first fmul operand; the
+ *      scaled moments have no other use). r01 pinned all of this unfused.
  *   Everything else is the reference expression, evaluated left to right in
  *   IEEE fp32 with no FMA contraction (-ffp-contract=off).
  *
@@ -430,11 +435,13 @@ static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const 
             const float src_pix = tex_bilinear(simg, sW, sH, sp.x, sp.y, prm->texture_filter8);
             float w = ComputeBilateralWeight((float)i, (float)j, ref_pix, ref_center,
                                              prm->sigma_spatial, prm->sigma_color);
+            /* pin P3: nvcc's default contraction (--fmad=true, implied by the
+             * reference's --use_fast_math) fuses every `sum += a * b` here */
             const float wr = w * ref_pix;
             const float ws = w * src_pix;
-            r_ref += wr;
+            r_ref = dm_fma(w, ref_pix, r_ref);
             r_rr = dm_fma(wr, ref_pix, r_rr);
-            r_src += ws;
+            r_src = dm_fma(w, src_pix, r_src);
             r_ss = dm_fma(ws, src_pix, r_ss);
             r_rs = dm_fma(wr, src_pix, r_rs);
             r_w += w;
@@ -448,15 +455,16 @@ static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const 
     }
     const float inv = 1.0f / bw_sum;
     sum_ref *= inv;
-    sum_ref_ref *= inv;
     sum_src *= inv;
-    sum_src_src *= inv;
-    sum_ref_src *= inv;
-    const float var_ref = sum_ref_ref - sum_ref * sum_ref;
-    const float var_src = sum_src_src - sum_src * sum_src;
+    /* ... and each `sum_xy * inv - m_x * m_y` (the scaled moment being the
+     * first operand) into fma(sum_xy, inv, -(m_x * m_y)). On a flat patch this
+     * leaves var, covar as independent residuals instead of three equal ones,
+     * which decides the kMinVar test and the cost there. */
+    const float var_ref = dm_fma(sum_ref_ref, inv, -(sum_ref * sum_ref));
+    const float var_src = dm_fma(sum_src_src, inv, -(sum_src * sum_src));
     const float kMinVar = 1e-5f;
     if (var_ref < kMinVar || var_src < kMinVar) return cost_max;
-    const float covar = sum_ref_src - sum_ref * sum_src;
+    const float covar = dm_fma(sum_ref_src, inv, -(sum_ref * sum_src));
     const float var_rs = dm_sqrt(var_ref * var_src);
     float c = 1.0f - covar / var_rs;
     c = (c < cost_max) ? c : cost_max;   /* min(cost_max, .) : NaN -> cost_max */
