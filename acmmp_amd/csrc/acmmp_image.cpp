@@ -7,6 +7,9 @@
 //    ISLOW integer IDCT with its range-limit table, Y taken without colour
 //    conversion. Progressive / arithmetic / 12-bit files are rejected
 //    (ACMMP_ERR_UNSUPPORTED).
+//    The IDCT algorithm and its constants (the Loeffler-Ligtenberg-Moschytz
+//    factorisation as laid out in jidctint.c) are the Independent JPEG
+//    Group's; this file re-implements them, it contains no IJG source.
 //  * binary PGM (P5, 8/16-bit) and grayscale PFM as lossless alternatives.
 //  * cv::resize(..., INTER_LINEAR) of a float image (src/ACMMP.cpp:578-597),
 //    including OpenCV's switch to INTER_AREA for exact 2x downscales.

@@ -718,6 +718,19 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
+// ------------------------------------------------- diagnostic phase stamps
+// ACMMP_DIAG_STAMPS builds only (never the product library): per-phase
+// s_memtime cycle sums of the sweep kernel, accumulated by lane 0 of each wave.
+#ifdef ACMMP_DIAG_STAMPS
+__device__ unsigned long long g_diag_cycles[24];
+#define DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(slot, a, b) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[slot], (b) - (a)); } while (0)
+#else
+#define DIAG_T(var)
+#define DIAG_ADD(slot, a, b)
+#endif
+
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
 // wave-uniform). Reference samples come from the LDS tile, source samples
 // through ncc_sums.
@@ -748,6 +761,36 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
+#ifdef ACMMP_DIAG_STAMPS
+    {  // coherence census: the wave's bounding box of footprint records over
+       // the active lanes' patches (corner projections, +1 record margin);
+       // slot 13/14/15 += active lanes whose wave box fits 512 / 2048 / 8192
+       // records, slot 16 += all active lanes (0 when the window test fails)
+        float bx0 = 1e30f, bx1 = -1e30f, by0 = 1e30f, by1 = -1e30f;
+        const float cxs[2] = {xl, xr}, cys[2] = {yt, yb};
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 2; ++b) {
+                const float2 q = project(H, cxs[a], cys[b]);
+                const float qx = fminf(fmaxf(q.x, -1.0f), (float)im.W), qy = fminf(fmaxf(q.y, -1.0f), (float)im.H);
+                bx0 = fminf(bx0, floorf(qx)); bx1 = fmaxf(bx1, floorf(qx));
+                by0 = fminf(by0, floorf(qy)); by1 = fmaxf(by1, floorf(qy));
+            }
+        const unsigned ux0 = (unsigned)(bx0 + 2.0f), ux1 = (unsigned)(bx1 + 2.0f);
+        const unsigned uy0 = (unsigned)(by0 + 2.0f), uy1 = (unsigned)(by1 + 2.0f);
+        const unsigned wx0 = __builtin_amdgcn_wave_reduce_min_u32(ux0, 1), wx1 = __builtin_amdgcn_wave_reduce_max_u32(ux1, 1);
+        const unsigned wy0 = __builtin_amdgcn_wave_reduce_min_u32(uy0, 1), wy1 = __builtin_amdgcn_wave_reduce_max_u32(uy1, 1);
+        const unsigned long long area = (unsigned long long)(wx1 - wx0 + 3) * (wy1 - wy0 + 3);
+        const unsigned long long act = __builtin_popcountll(__builtin_amdgcn_read_exec());
+        const bool first = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+                           (unsigned)__builtin_ctzll(__builtin_amdgcn_read_exec());
+        if (first) {
+            if (fast && area <= 512) atomicAdd(&g_diag_cycles[13], act);
+            if (fast && area <= 2048) atomicAdd(&g_diag_cycles[14], act);
+            if (fast && area <= 8192) atomicAdd(&g_diag_cycles[15], act);
+            atomicAdd(&g_diag_cycles[16], act);
+        }
+    }
+#endif
     if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
 #else
@@ -902,19 +945,6 @@ DEV float4 upscale_normal(const KViews &kv, const KState &st, int px, int py, fl
     normalize3(n_total);
     return n_total;
 }
-
-// ------------------------------------------------- diagnostic phase stamps
-// ACMMP_DIAG_STAMPS builds only (never the product library): per-phase
-// s_memtime cycle sums of the sweep kernel, accumulated by lane 0 of each wave.
-#ifdef ACMMP_DIAG_STAMPS
-__device__ unsigned long long g_diag_cycles[16];
-#define DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
-#define DIAG_ADD(slot, a, b) \
-    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[slot], (b) - (a)); } while (0)
-#else
-#define DIAG_T(var)
-#define DIAG_ADD(slot, a, b)
-#endif
 
 // ------------------------------------------------------ colour-split lanes
 // Every PatchMatch kernel maps a 64x4 block onto 64 colour-split columns x 4
@@ -1999,9 +2029,9 @@ hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t 
 
 int diag_read_cycles(unsigned long long *out8) {
 #ifdef ACMMP_DIAG_STAMPS
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 16 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 24 * sizeof(unsigned long long)) != hipSuccess)
         return -3;
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_cycles), z, sizeof(z)) != hipSuccess) return -3;
     return 0;
 #else

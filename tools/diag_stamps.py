@@ -14,7 +14,7 @@ imgs = [scene.render_torch(setup, i, dev) for i in ids]
 eng = ACMMP(0); p = default_params(); p.max_iterations = 8; eng.set_params(p)
 eng.set_images_device([setup.camera(i) for i in ids], [im.data_ptr() for im in imgs])
 eng.RunPatchMatch()
-out = (C.c_uint64 * 16)(); fn(out)  # reset after warmup
+out = (C.c_uint64 * 24)(); fn(out)  # reset after warmup
 eng.RunPatchMatch()
 fn(out)
 names = ["tile+search", "pixel_patch", "phaseA_ncc(8 dirs x views)", "view_select+final_costs", "current+refine(6 x sel views)"]
@@ -24,3 +24,5 @@ print(json.dumps({"candidates": out[5], "dup_of_earlier_candidate": out[6] / max
                   "equal_to_current_plane": out[7] / max(out[5], 1),
                   "unique_per_lane": out[11] / max(out[1 + 9] * 64, 1), "wave_max_unique": out[12] / max(out[10], 1),
                   "sel_views_per_lane": out[9] / max(out[10] * 64, 1), "sel_views_wave_union": out[8] / max(out[10], 1)}))
+print(json.dumps({"ncc_lane_calls": out[16], "wave_box_le_512": out[13] / max(out[16], 1),
+                  "wave_box_le_2048": out[14] / max(out[16], 1), "wave_box_le_8192": out[15] / max(out[16], 1)}))
