@@ -296,6 +296,13 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
             "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 "
                     "(Infinity-Cache hits included), FETCH doubled per the gfx950 calibration",
         },
+        "valu": {
+            "bound": "valu",
+            "frac": round(pmc["valu_busy_frac"], 4),
+            "insts": round(pmc["valu_insts"]),
+            "note": "share of SIMD cycles issuing VALU (4 x SQ_ACTIVE_INST_VALU quad-cycles / (1024 SIMDs x "
+                    "GRBM_GUI_ACTIVE/8)): the kernel is co-bound by the TD gather path (frac) and the VALU",
+        },
         "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
     })
     return out

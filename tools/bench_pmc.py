@@ -18,6 +18,11 @@ Derived per k_sweep launch (mean over the step's launches):
                    (GRBM_GUI_ACTIVE is summed over the 8 XCDs; one TD per CU)
   gather_insts   = TA_BUFFER_READ_WAVEFRONTS_sum (buffer_load wave-instructions)
   td_cyc_per_inst = TD_TD_BUSY_sum / gather_insts
+  valu_busy_frac = 4 * SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / XCDS * CUS * 4)
+                   (the counter is in quad-cycles summed over waves; 4 SIMDs per
+                   CU, one VALU issue per SIMD: the share of SIMD cycles that
+                   execute VALU, the second roofline of this kernel)
+  valu_insts     = SQ_INSTS_VALU (wave-instructions)
   duration_ms    = kernel-trace end - start of the same dispatches (profiled;
                    bench.py reports its own un-profiled HIP-event duration too)
 """
@@ -38,7 +43,8 @@ XCDS = 8
 PASSES = [
     ("fetch", ["FETCH_SIZE", "GRBM_GUI_ACTIVE", "TD_TD_BUSY_sum", "TA_BUFFER_READ_WAVEFRONTS_sum",
                "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVES"]),
-    ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "SQ_INSTS_VMEM_WR"]),
+    ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_VALU",
+               "SQ_INSTS_VALU"]),
 ]
 
 
@@ -125,6 +131,8 @@ def summarize(res: dict) -> dict:
         "vmem_wr_insts": mean(w, "SQ_INSTS_VMEM_WR"),
         "lds_insts": mean(f, "SQ_INSTS_LDS"),
         "waves": mean(f, "SQ_WAVES"),
+        "valu_insts": mean(w, "SQ_INSTS_VALU"),
+        "valu_busy_frac": 4 * mean(w, "SQ_ACTIVE_INST_VALU") / ((mean(w, "GRBM_GUI_ACTIVE") / XCDS) * CUS * 4),
         "gpu_cycles_per_xcd": cyc_per_cu,
         "profiled_ms": statistics.mean(durs) if durs else float("nan"),
         "clock_ghz": cyc_per_cu / (statistics.mean(durs) * 1e6) if durs else float("nan"),
