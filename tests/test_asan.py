@@ -6,6 +6,7 @@ on valid inputs and on deterministic mutations of them (byte flips,
 truncations, extreme header fields, duplicated / inserted ranges). Any
 sanitizer report fails the test. CPU only; the GPU kernels are covered by the
 -m gpu parity suite (GPU sanitizers are not available on the pool)."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -27,7 +28,12 @@ pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ with li
 
 @pytest.fixture(scope="module")
 def driver():
-    r = subprocess.run(["make", "-s", "-C", ASAN_DIR], capture_output=True, text=True, timeout=600)
+    # one make at a time (pytest-xdist workers would otherwise relink the
+    # driver while another worker executes it: ETXTBSY)
+    os.makedirs(os.path.join(ASAN_DIR, "build"), exist_ok=True)
+    with open(os.path.join(ASAN_DIR, "build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", ASAN_DIR], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     return DRIVER
 
