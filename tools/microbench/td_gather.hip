@@ -45,6 +45,13 @@ __global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, i
             case 14: idx = base + (lane >> 2) + 64 * (s & 7); break;                   // lane quads share a record
             case 15: idx = base + 3 * lane + (s & 7); break;                            // stride 3 (12 B)
             case 16: idx = base + 8 * lane + (s & 7); break;                            // stride 8 (32 B): 4 lanes/line
+            case 17: case 18: case 19: case 20: {  // k_sweep 8x8 colour-split wave: 16 px x 8 rows,
+                // in a linear (17), 16x2 (18), 8x4 (19) or 4x8 (20) record-tiled layout (128-B lines)
+                const int cc = lane & 7, rr = lane >> 3;
+                const int x = 64 + 2 * cc + (rr & 1) + (s % 6) * 2 + (wave % 13), y = (wave % 64) * 8 + rr + (s / 6) * 2;
+                const int tw = pattern == 17 ? 32 : pattern == 18 ? 16 : pattern == 19 ? 8 : 4, th = 32 / tw;
+                idx = ((y / th) * (PITCH / tw) + x / tw) * 32 + (y % th) * tw + (x % tw);
+            } break;
             default: idx = base + lane * 33; break;                                     // one line per lane
         }
         const bool on = pattern == 8 || pattern == 12 ? (lane & 3) == 0
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, i
 }
 
 int main(int argc, char **argv) {
-    const int nrec = PITCH * 600;
+    const int nrec = PITCH * 640;
     unsigned *buf, *out;
     (void)hipMalloc(&buf, (size_t)nrec * 4);
     (void)hipMalloc(&out, 4);
@@ -67,7 +74,7 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int p = 0; p < 17; ++p) {
+    for (int p = 0; p < 21; ++p) {
         for (int rep = 0; rep < 3; ++rep) {
             (void)hipEventRecord(a);
             k_gather<<<blocks, 256>>>(buf, nrec, p, out);
