@@ -55,6 +55,10 @@ constexpr int kTaps = 6;
 #ifndef ACMMP_PIPE_ROWS
 #define ACMMP_PIPE_ROWS 1
 #endif
+// u8 footprints: the two samples of a column pair lerped as packed pairs
+#ifndef ACMMP_PACKED_LERP
+#define ACMMP_PACKED_LERP 1
+#endif
 // view selection's CDF and the photometric final costs with static indices
 #ifndef ACMMP_SELECT_REGS
 #define ACMMP_SELECT_REGS 1
@@ -612,8 +616,23 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
                                __builtin_fmaf(rf.ax[p].y, (float)db.y, (float)tb.y)};
             sv = fma2(rf.ay[p], r1 - r0, r0);
         } else if (U8) {
+#if ACMMP_PACKED_LERP
+            // lerp_sample's operations with the pair's two samples in the two
+            // components (sample a in .x, b in .y, as ax / ay already are):
+            // top = fma(ax, t10 - t00, t00), bot = fma(ax, t11 - t01, t01),
+            // fma(ay, bot - top, top) — 6 packed ops per pair instead of 8
+            const unsigned qa = rf.q[2 * p], qb = rf.q[2 * p + 1];
+            const f2v t00 = f2v{(float)(qa & 0xffu), (float)(qb & 0xffu)};
+            const f2v t01 = f2v{(float)((qa >> 8) & 0xffu), (float)((qb >> 8) & 0xffu)};
+            const f2v t10 = f2v{(float)((qa >> 16) & 0xffu), (float)((qb >> 16) & 0xffu)};
+            const f2v t11 = f2v{(float)(qa >> 24), (float)(qb >> 24)};
+            const f2v top = fma2(rf.ax[p], t10 - t00, t00);
+            const f2v bot = fma2(rf.ax[p], t11 - t01, t01);
+            sv = fma2(rf.ay[p], bot - top, top);
+#else
             sv = f2v{lerp_sample(unpack_quad(rf.q[2 * p]), rf.ax[p].x, rf.ay[p].x),
                      lerp_sample(unpack_quad(rf.q[2 * p + 1]), rf.ax[p].y, rf.ay[p].y)};
+#endif
         } else {
             sv = f2v{lerp_sample(rf.t[2 * p], rf.ax[p].x, rf.ay[p].x),
                      lerp_sample(rf.t[2 * p + 1], rf.ax[p].y, rf.ay[p].y)};
