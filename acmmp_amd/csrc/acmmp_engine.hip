@@ -218,10 +218,27 @@ int set_depths_impl(acmmp_ctx *ctx, const float *const *depths, const int32_t *p
 // Records per row and bytes of one view's padded footprint records in
 // `form` (128-B rows: u8 quads W + 2, f16 quads W + 2, fp32 row pairs
 // W + 3; sized for the fp32 form, the largest). Non-zero: too large.
+// Row skew of the compact forms, in records (ACMMP_PAD_SKEW, 0..64): the
+// u8 / h16 row pitch is rounded to whole 128-B lines and then offset by the
+// skew, so consecutive record rows start at different offsets within a line.
+#ifndef ACMMP_PAD_SKEW_DEFAULT
+#define ACMMP_PAD_SKEW_DEFAULT 0
+#endif
+int pad_skew() {
+    static const int skew = [] {
+        const char *e = std::getenv("ACMMP_PAD_SKEW");
+        const int v = e ? std::atoi(e) : ACMMP_PAD_SKEW_DEFAULT;
+        return v < 0 ? 0 : (v > 64 ? 64 : v);
+    }();
+    return skew;
+}
+
 int pad_geometry(int w, int h, int form, int &pp, size_t &bytes) {
     const int pf = (w + 3 + 15) / 16 * 16;
     pp = form == kTexelU8 ? (w + 2 + 31) / 32 * 32 : form == kTexelH16 ? (w + 2 + 15) / 16 * 16 : pf;
-    bytes = (size_t)pf * (h + 2) * 2 * sizeof(float);
+    if (form != kTexelF32) pp += pad_skew();
+    const size_t rec = form == kTexelU8 ? 4 : 8;
+    bytes = std::max((size_t)pf * (h + 2) * 2 * sizeof(float), (size_t)pp * (h + 2) * rec);
     // the gather kernels index records with a 24x24-bit multiply into a
     // signed 32-bit record index (kv_upload picks the fp32 form below 2^24)
     return ((size_t)pf * (h + 2) >= (1u << 31) || pf >= (1 << 24) || h + 2 >= (1 << 24)) ? 1 : 0;

@@ -52,6 +52,13 @@ __global__ __launch_bounds__(256) void k_gather(const unsigned *buf, int nrec, i
                 const int tw = pattern == 17 ? 32 : pattern == 18 ? 16 : pattern == 19 ? 8 : 4, th = 32 / tw;
                 idx = ((y / th) * (PITCH / tw) + x / tw) * 32 + (y % th) * tw + (x % tw);
             } break;
+            case 21: case 22: case 23: case 24: case 25: {  // pattern 17 with the row pitch 1632 +
+                // 1, 4, 8, 16, 24 records (rows no longer all start at the same offset in a 128-B line)
+                const int cc = lane & 7, rr = lane >> 3;
+                const int x = 64 + 2 * cc + (rr & 1) + (s % 6) * 2 + (wave % 13), y = (wave % 64) * 8 + rr + (s / 6) * 2;
+                const int d = pattern == 21 ? 1 : pattern == 22 ? 4 : pattern == 23 ? 8 : pattern == 24 ? 16 : 24;
+                idx = y * (PITCH + d) + x;
+            } break;
             default: idx = base + lane * 33; break;                                     // one line per lane
         }
         const bool on = pattern == 8 || pattern == 12 ? (lane & 3) == 0
@@ -74,7 +81,7 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int p = 0; p < 21; ++p) {
+    for (int p = 0; p < 26; ++p) {
         for (int rep = 0; rep < 3; ++rep) {
             (void)hipEventRecord(a);
             k_gather<<<blocks, 256>>>(buf, nrec, p, out);
