@@ -225,12 +225,9 @@ int set_depths_impl(acmmp_ctx *ctx, const float *const *depths, const int32_t *p
 #define ACMMP_PAD_SKEW_DEFAULT 0
 #endif
 int pad_skew() {
-    static const int skew = [] {
-        const char *e = std::getenv("ACMMP_PAD_SKEW");
-        const int v = e ? std::atoi(e) : ACMMP_PAD_SKEW_DEFAULT;
-        return v < 0 ? 0 : (v > 64 ? 64 : v);
-    }();
-    return skew;
+    const char *e = std::getenv("ACMMP_PAD_SKEW");
+    const int v = e ? std::atoi(e) : ACMMP_PAD_SKEW_DEFAULT;
+    return v < 0 ? 0 : (v > 64 ? 64 : v);
 }
 
 int pad_geometry(int w, int h, int form, int &pp, size_t &bytes) {

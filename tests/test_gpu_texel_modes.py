@@ -56,6 +56,19 @@ def test_every_texel_form_matches_oracle(prob, monkeypatch, form, bits):
     _check(prm, cams, imgs, pl, co, sv, f"{bits}-bit texels")
 
 
+@pytest.mark.parametrize("form,bits", [("u8", 8), ("h16", 16)])
+@pytest.mark.parametrize("skew", [1, 5, 16])
+def test_skewed_record_rows_match_oracle(prob, monkeypatch, form, bits, skew):
+    """ACMMP_PAD_SKEW offsets the compact forms' row pitch by whole records
+    (rows no longer start on a 128-B line): a layout change only."""
+    cams, imgs = prob
+    monkeypatch.setenv("ACMMP_TEXEL", form)
+    monkeypatch.setenv("ACMMP_PAD_SKEW", str(skew))
+    got, prm, pl, co, sv = _run(cams, imgs)
+    assert got == bits
+    _check(prm, cams, imgs, pl, co, sv, f"{bits}-bit texels, row skew {skew}")
+
+
 def test_texel_f32_switch(prob, monkeypatch):
     cams, imgs = prob
     monkeypatch.setenv("ACMMP_TEXEL_F32", "1")
