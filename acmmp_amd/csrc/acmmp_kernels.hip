@@ -688,7 +688,23 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
     f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
-#if ACMMP_PIPE_ROWS
+#if ACMMP_PIPE_ROWS == 2
+    // two rows in flight ahead of the one being reduced (three rotating
+    // fetch buffers, the six rows straight-line)
+    RowFetch<TX> ra, rb, rc;
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 1, rb);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 2, rc);
+    reduce_row<TX>(ra, wl, rt, wstride, 0, acc_s, acc_ss, acc_rs);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 3, ra);
+    reduce_row<TX>(rb, wl, rt, wstride, 1, acc_s, acc_ss, acc_rs);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 4, rb);
+    reduce_row<TX>(rc, wl, rt, wstride, 2, acc_s, acc_ss, acc_rs);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 5, rc);
+    reduce_row<TX>(ra, wl, rt, wstride, 3, acc_s, acc_ss, acc_rs);
+    reduce_row<TX>(rb, wl, rt, wstride, 4, acc_s, acc_ss, acc_rs);
+    reduce_row<TX>(rc, wl, rt, wstride, 5, acc_s, acc_ss, acc_rs);
+#elif ACMMP_PIPE_ROWS
     // two rows per trip (ping-pong fetch buffers, no register copies)
     RowFetch<TX> ra, rb;
     fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
