@@ -371,6 +371,20 @@ static_assert(kBX * kBY == 256 && (kBX == 64 || kBX == 32 || kBX == 16 || kBX ==
 // (A tile pitch of 16 mod 32 floats, which puts the two 16-lane rows of a
 // ds_read2_b32 lane group on disjoint banks, measured 0.3 % faster: not kept.)
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
+// ACMMP_TILE_SKEW=1: tile rows stored with pitch kTileP = 8 (mod 32) floats
+// and each row shifted by the colour parity of its samples, so a lane's
+// sample address carries no parity term: the 4 wave rows x 8 lanes of a
+// 32-lane ds_read group land on 32 distinct banks (pitch 22 with the
+// per-row parity offset gave 2-way conflicts).
+#ifndef ACMMP_TILE_SKEW
+#define ACMMP_TILE_SKEW 0
+#endif
+#if ACMMP_TILE_SKEW
+constexpr int kTileP = ((kTileW + 1 + 23) / 32) * 32 + 8;  // >= kTileW + 1, = 8 mod 32
+static_assert(kTileP >= kTileW + 1 && kTileP % 32 == 8, "tile pitch");
+#else
+constexpr int kTileP = kTileW;
+#endif
 
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
     const float *img = kv.img[0];
@@ -379,8 +393,13 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
         const int r = e / kTileW, kk = e - r * kTileW;
         const int yy = y0 - 5 + r;
         const int kc = k0 - 3 + kk;
-        const int xx = 2 * kc + ((yy + colour) & 1);
+        const int par = (yy + colour) & 1;
+        const int xx = 2 * kc + par;
+#if ACMMP_TILE_SKEW
+        tile[r * kTileP + kk + par] = texel(img, pitch, W, H, xx, yy);
+#else
         tile[e] = texel(img, pitch, W, H, xx, yy);
+#endif
     }
 }
 
@@ -436,14 +455,18 @@ DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, 
 // tb = tile index of sample (ii=0, jj=0) of this lane: ty*kTileW + tx + s
 DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatch &pp) {
     const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
+#if ACMMP_TILE_SKEW
+    const float center = tile[tb + 5 * kTileP + 2 + s];
+#else
     const float center = tile[tb - s + 5 * kTileW + 3];
+#endif
     float sum_ref = 0.0f, sum_rr = 0.0f, bw = 0.0f;
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
         float r_ref = 0.0f, r_rr = 0.0f, r_w = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const float r = tile[tb + ii + 2 * kTileW * jj];
+            const float r = tile[tb + ii + 2 * kTileP * jj];
             const float w = bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
             const float wr = w * r;
             r_ref = dm_fma(w, r, r_ref);  // nvcc's contraction of `sum += w * r` (pin P3)
@@ -645,7 +668,7 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
 #else
         const WSlot w = wl[wslot(p, jj) * wstride];
 #if !ACMMP_LDS_WR
-        const float *rr = rt + 2 * kTileW * jj + 2 * p;
+        const float *rr = rt + 2 * kTileP * jj + 2 * p;
 #endif
 #endif
         const f2v wv = f2v{w.x, w.y};
@@ -1032,7 +1055,11 @@ DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     g.py = b.by * kBY + ty;
     g.s = (g.py + colour) & 1;
     g.px = 2 * g.k + g.s;
+#if ACMMP_TILE_SKEW
+    g.tb = ty * kTileP + tx + 1;
+#else
     g.tb = ty * kTileW + tx + g.s;
+#endif
     return g;
 }
 
@@ -1043,7 +1070,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, t
 // writes the colour-split "current" buffers. blockIdx.z = colour.
 template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
-    __shared__ float tile[kTileW * kTileH];
+    __shared__ float tile[kTileP * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
@@ -1234,7 +1261,7 @@ template <int NS, int TX, int MODE>
 DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int iter) {
     static_assert(MODE == 0 || (ACMMP_CAND_LDS && ACMMP_COMPACT_REFINE && ACMMP_SELECT_REGS),
                   "the split sweep is built on the default variants");
-    __shared__ float tile[kTileW * kTileH];
+    __shared__ float tile[kTileP * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
 #if ACMMP_CAND_LDS
     __shared__ float4 cand_lds[8 * kThreads];
@@ -1943,7 +1970,7 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
 template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
-    __shared__ float tile[kTileW * kTileH];
+    __shared__ float tile[kTileP * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
