@@ -196,6 +196,7 @@ SIGNATURES = {
     "acmmp_get_texel_bits": (C.c_int, [_CTX]),
     "acmmp_device_count": (C.c_int, []),
     "acmmp_version": (C.c_char_p, []),
+    "acmmp_host_threads": (C.c_int, []),
     "acmmp_generate_sample_list": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
     "acmmp_compute_multiscale_settings": (C.c_int, [C.c_char_p, C.POINTER(Problem), C.c_int, C.POINTER(C.c_int)]),
     "acmmp_input_initialization": (C.c_int, [_CTX, C.c_char_p, C.c_char_p, C.POINTER(Problem), C.c_int, C.c_int]),

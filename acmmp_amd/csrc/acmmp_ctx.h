@@ -26,6 +26,7 @@ struct acmmp_texture {
     int W = 0, H = 0;
     int form = 0;                // kTexelF32 / kTexelU8 / kTexelH16
     float *pad = nullptr;        // owned
+    size_t pad_bytes = 0;        // bytes allocated at pad
     int pad_pitch = 0;           // records per row
 };
 
@@ -66,8 +67,6 @@ struct acmmp_ctx {
     float4 *d_scaled = nullptr;
     size_t scaled_count = 0;
     float4 *d_seed = nullptr;
-    float *d_xsplit = nullptr;         // split sweep scratch (KState::xcost/xprob/xdesc), grow-only
-    size_t xsplit_count = 0;
     bool have_prior = false, have_scaled = false, have_seed = false, have_state = false;
 
     // Per-run constant block. A ring of pinned host / device slots so an

@@ -54,8 +54,6 @@ void free_state(acmmp_ctx *ctx) {
     dfree(ctx->d_mask);
     dfree(ctx->d_scaled);
     dfree(ctx->d_seed);
-    dfree(ctx->d_xsplit);
-    ctx->xsplit_count = 0;
     ctx->have_prior = ctx->have_scaled = ctx->have_seed = ctx->have_state = false;
 }
 
@@ -163,13 +161,6 @@ KState state_of(acmmp_ctx *ctx) {
     st.mask = ctx->d_mask;
     st.scaled = ctx->d_scaled;
     st.seed = ctx->d_seed;
-    st.xplane = (size_t)ctx->Wh * ctx->H;
-    if (ctx->d_xsplit) {
-        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
-        st.xcost = ctx->d_xsplit;
-        st.xprob = st.xcost + 8 * nv * st.xplane;
-        st.xdesc = reinterpret_cast<uint32_t *>(st.xprob + nv * st.xplane);
-    }
     return st;
 }
 
@@ -217,23 +208,11 @@ int set_depths_impl(acmmp_ctx *ctx, const float *const *depths, const int32_t *p
 
 // Records per row and bytes of one view's padded footprint records in
 // `form` (128-B rows: u8 quads W + 2, f16 quads W + 2, fp32 row pairs
-// W + 3; sized for the fp32 form, the largest). Non-zero: too large.
-// Row skew of the compact forms, in records (ACMMP_PAD_SKEW, 0..64): the
-// u8 / h16 row pitch is rounded to whole 128-B lines and then offset by the
-// skew, so consecutive record rows start at different offsets within a line.
-#ifndef ACMMP_PAD_SKEW_DEFAULT
-#define ACMMP_PAD_SKEW_DEFAULT 0
-#endif
-int pad_skew() {
-    const char *e = std::getenv("ACMMP_PAD_SKEW");
-    const int v = e ? std::atoi(e) : ACMMP_PAD_SKEW_DEFAULT;
-    return v < 0 ? 0 : (v > 64 ? 64 : v);
-}
-
+// W + 3; sized for the fp32 form, the largest, so one allocation serves
+// every form). Non-zero: too large.
 int pad_geometry(int w, int h, int form, int &pp, size_t &bytes) {
     const int pf = (w + 3 + 15) / 16 * 16;
     pp = form == kTexelU8 ? (w + 2 + 31) / 32 * 32 : form == kTexelH16 ? (w + 2 + 15) / 16 * 16 : pf;
-    if (form != kTexelF32) pp += pad_skew();
     const size_t rec = form == kTexelU8 ? 4 : 8;
     bytes = std::max((size_t)pf * (h + 2) * 2 * sizeof(float), (size_t)pp * (h + 2) * rec);
     // the gather kernels index records with a 24x24-bit multiply into a
@@ -559,9 +538,15 @@ int acmmp_texture_create(int device, const float *d_image, int pitch, int width,
             rc = ACMMP_ERR_UNSUPPORTED;
             break;
         }
-        if (!t->pad && hipMalloc((void **)&t->pad, bytes) != hipSuccess) {
-            rc = ACMMP_ERR_HIP;
-            break;
+        if (bytes > t->pad_bytes) {  // every form's bytes, not only the first tried
+            if (t->pad) (void)hipFree(t->pad);
+            t->pad = nullptr;
+            t->pad_bytes = 0;
+            if (hipMalloc((void **)&t->pad, bytes) != hipSuccess) {
+                rc = ACMMP_ERR_HIP;
+                break;
+            }
+            t->pad_bytes = bytes;
         }
         uint32_t unfit = 0;
         if (hipMemsetAsync(d_unfit, 0, sizeof(uint32_t), s) != hipSuccess ||
@@ -770,17 +755,6 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
-    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
-        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
-        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
-        if (need > ctx->xsplit_count) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
-            dfree(ctx->d_xsplit);
-            ctx->xsplit_count = 0;
-            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
-            ctx->xsplit_count = need;
-        }
-    }
     if (p.texture_filter8 && (ctx->pad_texel == kTexelH16 || ctx->h_kv.wide))
         return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "texture_filter8 is built for the u8 / fp32 texel forms below 2^24 records");
     if (ctx->timing && !ctx->events_made) {
@@ -898,17 +872,6 @@ int acmmp_eval_costs(acmmp_ctx *ctx, const float *planes4, float *out_costs, flo
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
-    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
-        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
-        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
-        if (need > ctx->xsplit_count) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
-            dfree(ctx->d_xsplit);
-            ctx->xsplit_count = 0;
-            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
-            ctx->xsplit_count = need;
-        }
-    }
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;
     float4 *d_pl = nullptr;
@@ -942,17 +905,6 @@ int acmmp_eval_geom_costs(acmmp_ctx *ctx, const float *planes4, float *out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     rc = kv_upload(ctx);
     if (rc) return rc;
-    if (kSplitSweep) {  // phase A -> selection + refinement hand-off planes
-        const size_t nv = (size_t)std::max(ctx->n - 1, 1);
-        const size_t need = (9 * nv + 9) * (size_t)ctx->Wh * ctx->H;
-        if (need > ctx->xsplit_count) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // a queued run may still use the old one
-            dfree(ctx->d_xsplit);
-            ctx->xsplit_count = 0;
-            HIP_TRY(ctx, dalloc(ctx->d_xsplit, need));
-            ctx->xsplit_count = need;
-        }
-    }
     const size_t P = (size_t)ctx->W * ctx->H;
     const int ns = ctx->n - 1;
     float4 *d_pl = nullptr;
@@ -1033,11 +985,6 @@ int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checke
     }
     (void)hipFree(d);
     return rc;
-}
-
-// Diagnostic builds only (ACMMP_DIAG_STAMPS); not declared in include/acmmp.h.
-int acmmp_diag_read_cycles(uint64_t *out8) {
-    return out8 ? diag_read_cycles((unsigned long long *)out8) : ACMMP_ERR_ARG;
 }
 
 int acmmp_set_timing(acmmp_ctx *ctx, int enable) {

@@ -93,11 +93,11 @@ float get_angle(const float *a, const float *b) {  // GetAngle
     return angle;
 }
 
-// Runs fn(0..n-1) on up to 16 host threads; returns the status of the lowest
+// Runs fn(0..n-1) on acmmp_host_threads() threads; returns the status of the lowest
 // failing index with its message (what the sequential loop reports first).
 template <class Fn>
 int parallel_for(int n, Fn fn) {
-    const int workers = std::min<int>(n, (int)std::min(std::max(1u, std::thread::hardware_concurrency()), 16u));
+    const int workers = std::min<int>(n, acmmp_host_threads());
     std::vector<int> rc((size_t)std::max(n, 0), ACMMP_OK);
     std::vector<std::string> msg(rc.size());
     std::atomic<int> next{0};

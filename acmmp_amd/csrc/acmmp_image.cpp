@@ -353,8 +353,9 @@ void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) 
         int64_t z1 = (z2 + z3) * F0541;
         int64_t tmp2 = z1 + z3 * (-F1847);
         int64_t tmp3 = z1 + z2 * F0765;
-        int64_t tmp0 = (w[0] + w[4]) * ((int64_t)1 << kConstBits);
-        int64_t tmp1 = (w[0] - w[4]) * ((int64_t)1 << kConstBits);
+        // operands widened before the sum, as libjpeg-turbo's (JLONG)wsptr[0] + (JLONG)wsptr[4]
+        int64_t tmp0 = ((int64_t)w[0] + w[4]) * ((int64_t)1 << kConstBits);
+        int64_t tmp1 = ((int64_t)w[0] - w[4]) * ((int64_t)1 << kConstBits);
         const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
         tmp0 = w[7];
         tmp1 = w[5];

@@ -78,23 +78,7 @@ struct KState {
     const uint32_t *mask;   // planar prior triangle labels
     const float4 *scaled;   // hierarchy low-res planes (scaled_rows x scaled_cols)
     const float4 *seed;     // seeded priors
-    // split sweep (kSplitSweep): phase A's results for the selection +
-    // refinement kernel, one plane of H * Wh per slot, indexed by the
-    // colour-split pixel index: xcost slot d * nsrc + v = cost of candidate d
-    // in view v; xprob slot v = view-selection probability; xdesc slots 0..7
-    // = the candidates' colour-split indices, slot 8 = flags | same << 8
-    float *xcost;
-    float *xprob;
-    uint32_t *xdesc;
-    size_t xplane;
 };
-
-// ACMMP_SPLIT=1: each half-sweep is two launches (phase A with fewer live
-// registers and more waves per SIMD; then selection + refinement)
-#ifndef ACMMP_SPLIT
-#define ACMMP_SPLIT 0
-#endif
-constexpr bool kSplitSweep = ACMMP_SPLIT != 0;
 
 // Kernel launchers (acmmp_kernels.hip). All enqueue on `stream`.
 hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream);
@@ -120,7 +104,6 @@ hipError_t launch_pad_h16(const float *src, int spitch, int W, int H, void *dst,
 // integer in [0, 255] (the copy is then unusable and the fp32 form is built).
 hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t *dst, int dpitch,
                            uint32_t *not_u8, hipStream_t stream);
-int diag_read_cycles(unsigned long long *out8);
 hipError_t launch_depth_planes(const float *depth, size_t n, float4 *out, hipStream_t stream);
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);

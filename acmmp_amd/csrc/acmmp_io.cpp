@@ -3,14 +3,53 @@
 //   read/writeDepthDmb    src/ACMMP.cpp:264-321
 //   read/writeNormalDmb   src/ACMMP.cpp:323-380
 // .dmb = int32 type(=1), h, w, nb, then h*w*nb little-endian float32 (HWC).
+#include <sched.h>
+
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <thread>
 
 #include "../../include/acmmp.h"
 
+namespace {
+// ceil(quota / period) of the cgroup CPU controller, 0 when unlimited/absent
+int cgroup_cpus() {
+    long long q = -1, p = 0;
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "max 100000" / "Q P"
+        char qs[32] = {0};
+        if (std::fscanf(f, "%31s %lld", qs, &p) == 2 && std::strcmp(qs, "max") != 0) q = std::atoll(qs);
+        std::fclose(f);
+    } else if (FILE *f1 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // v1
+        if (std::fscanf(f1, "%lld", &q) != 1) q = -1;
+        std::fclose(f1);
+        if (FILE *f2 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(f2, "%lld", &p) != 1) p = 0;
+            std::fclose(f2);
+        }
+    }
+    if (q <= 0 || p <= 0) return 0;
+    return (int)((q + p - 1) / p);
+}
+}  // namespace
+
 extern "C" {
+
+int acmmp_host_threads(void) {
+    if (const char *e = std::getenv("ACMMP_HOST_THREADS"))
+        if (std::atoi(e) > 0) return std::atoi(e);
+    int n = (int)std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = std::min(n, (int)CPU_COUNT(&set));
+    if (const int q = cgroup_cpus()) n = std::min(n, q);
+    if (const char *e = std::getenv("OMP_NUM_THREADS"))
+        if (std::atoi(e) > 0) n = std::min(n, std::atoi(e));
+    return std::max(n, 1);
+}
 
 int acmmp_read_camera(const char *path, acmmp_camera *cam) {
     if (!path || !cam) return ACMMP_ERR_ARG;

@@ -33,45 +33,13 @@ namespace acmmp {
 // offsets {-5,-3,-1,1,3,5}^2, src/ACMMP.h:34,37). The engine rejects others.
 constexpr int kTaps = 6;
 
-// Build options of the gather kernels (each an A/B-measured choice; the
-// defaults are the measured winners):
-//   ACMMP_BLOCK_X        colour-split columns per block (x 256/X rows)
-//   ACMMP_WAVE2D         rows of pixels per wave (lane_geom_of)
-//   ACMMP_CAND_LDS       the 8 candidate planes staged in LDS (k_sweep)
-//   ACMMP_COMPACT_REFINE refinement items packed across lanes (refine_costs_compact)
-//   ACMMP_PIPE_ROWS      software-pipelined patch rows (ncc_sums_rows)
-#ifndef ACMMP_WAVE2D
-#define ACMMP_WAVE2D 8
-#endif
-#ifndef ACMMP_CAND_LDS
-#define ACMMP_CAND_LDS 1
-#endif
-#ifndef ACMMP_COMPACT_REFINE
-#define ACMMP_COMPACT_REFINE 1
-#endif
-#if ACMMP_COMPACT_REFINE && !ACMMP_CAND_LDS
-#error "ACMMP_COMPACT_REFINE works in the LDS candidate slots (ACMMP_CAND_LDS=1)"
-#endif
-#ifndef ACMMP_PIPE_ROWS
-#define ACMMP_PIPE_ROWS 1
-#endif
-// u8 footprints: the two samples of a column pair lerped as packed pairs
-#ifndef ACMMP_PACKED_LERP
-#define ACMMP_PACKED_LERP 1
-#endif
-// view selection's CDF and the photometric final costs with static indices
-#ifndef ACMMP_SELECT_REGS
-#define ACMMP_SELECT_REGS 1
-#endif
-// Minimum waves per SIMD the sweep kernel is register-allocated for
-// (__launch_bounds__ 2nd argument; 2 -> <=256 VGPRs, 3 -> <=168, 4 -> <=128).
-#ifndef ACMMP_SWEEP_WAVES
-#define ACMMP_SWEEP_WAVES 2
-#endif
-// split sweep (ACMMP_SPLIT, acmmp_internal.h): waves per SIMD of its phase-A kernel
-#ifndef ACMMP_SPLIT_A_WAVES
-#define ACMMP_SPLIT_A_WAVES 3
-#endif
+// The kernel shapes below are the measured winners of the A/B experiments
+// recorded in DESIGN.md §4 (the rejected variants live in git history only):
+// 16 x 16 blocks of four 8 x 8-pixel waves, candidate planes staged in LDS,
+// refinement items packed across lanes, two software-pipelined patch rows,
+// packed-pair u8 lerps, view selection in registers, 2 waves per SIMD.
+constexpr int kWaveRows = 8;   // rows of pixels per wave (lane_geom_of)
+constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
 
 // ----------------------------------------------------------------- textures
 DEV float texel(const float *img, int pitch, int W, int H, int x, int y) {
@@ -263,18 +231,10 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
 }
 
 // Exactly rounded 1/z. The IEEE division sequence (v_div_scale / v_rcp /
-// 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. ACMMP_FAST_RCP
-// replaces it, inside the exponent window below, by v_rcp_f32 + one fma
-// Newton step — used only if acmmp_selftest_reciprocal() proves the two
-// bit-identical for EVERY float in that window on this hardware.
-// Software-pipeline the NCC sample loop one patch column ahead (1) or
-// fetch-then-reduce each column (0; fewer VGPRs, latency hidden by waves).
-#ifndef ACMMP_NCC_PIPELINE
-#define ACMMP_NCC_PIPELINE 1
-#endif
-#ifndef ACMMP_FAST_RCP
-#define ACMMP_FAST_RCP 1
-#endif
+// 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. Inside the
+// exponent window below the sample loop replaces it by v_rcp_f32 + one fma
+// Newton step, which acmmp_selftest_reciprocal() proves bit-identical for
+// EVERY float in that window on this hardware.
 DEV float recip_newton(float z) {
     const float r = __builtin_amdgcn_rcpf(z);
     const float e = dm_fma(-z, r, 1.0f);
@@ -285,13 +245,6 @@ DEV bool recip_fast_window(float z) {
     return az >= 0x1p-125f && az < 0x1p125f;
 }
 DEV float recip_exact(float z) { return 1.0f / z; }
-
-// FAST: v_rcp + Newton (caller guarantees z is inside recip_fast_window).
-template <bool FAST>
-DEV float recip(float z) {
-    if (FAST) return recip_newton(z);
-    return 1.0f / z;
-}
 
 // ComputeCorrespondingPoint (src/ACMMP.cu:324-331), pin P1
 DEV float2 project(const float *H, float x, float y) {
@@ -356,35 +309,15 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // colour-c plane, staged once in LDS (clamp-to-edge baked in); the address
 // of a sample is a compile-time offset from the lane's base.
 //
-// ACMMP_BLOCK_X = kBX: 16 (x 16 rows, the default) packs a block's four
-// waves (8 x 8 colour-split pixels each, ACMMP_WAVE2D) 2 x 2, so they share
-// most source-view rows of their patches in the CU's L1, and keeps the
-// ragged last block column narrow (Wh = 800 at 1600 px: 50 x 75 blocks;
-// 64 x 4 blocks gave 12.5 columns). cfg2, ms per k_sweep launch
-// (profiles/r02_block_shape.md): 64 x 4 blocks of 16 x 4 waves 4.66,
-// 32 x 8 4.41, 16 x 16 4.28, 16 x 16 of 8 x 8 waves 4.19, 8 x 32 4.18.
-#ifndef ACMMP_BLOCK_X
-#define ACMMP_BLOCK_X 16
-#endif
-constexpr int kBX = ACMMP_BLOCK_X, kBY = 256 / ACMMP_BLOCK_X;
-static_assert(kBX * kBY == 256 && (kBX == 64 || kBX == 32 || kBX == 16 || kBX == 8), "256-thread blocks");
-// (A tile pitch of 16 mod 32 floats, which puts the two 16-lane rows of a
-// ds_read2_b32 lane group on disjoint banks, measured 0.3 % faster: not kept.)
+// kBX = 16 colour-split columns x 16 rows packs a block's four waves (8 x 8
+// colour-split pixels each, kWaveRows) 2 x 2, so they share most
+// source-view rows of their patches in the CU's L1, and keeps the ragged
+// last block column narrow (Wh = 800 at 1600 px: 50 x 75 blocks). cfg2, ms
+// per k_sweep launch (profiles/r02_block_shape.md): 64 x 4 blocks of
+// 16 x 4 waves 4.66, 32 x 8 4.41, 16 x 16 4.28, 16 x 16 of 8 x 8 waves
+// 4.19, 8 x 32 4.18.
+constexpr int kBX = 16, kBY = 256 / kBX;
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
-// ACMMP_TILE_SKEW=1: tile rows stored with pitch kTileP = 8 (mod 32) floats
-// and each row shifted by the colour parity of its samples, so a lane's
-// sample address carries no parity term: the 4 wave rows x 8 lanes of a
-// 32-lane ds_read group land on 32 distinct banks (pitch 22 with the
-// per-row parity offset gave 2-way conflicts).
-#ifndef ACMMP_TILE_SKEW
-#define ACMMP_TILE_SKEW 0
-#endif
-#if ACMMP_TILE_SKEW
-constexpr int kTileP = ((kTileW + 1 + 23) / 32) * 32 + 8;  // >= kTileW + 1, = 8 mod 32
-static_assert(kTileP >= kTileW + 1 && kTileP % 32 == 8, "tile pitch");
-#else
-constexpr int kTileP = kTileW;
-#endif
 
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
     const float *img = kv.img[0];
@@ -395,11 +328,7 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
         const int kc = k0 - 3 + kk;
         const int par = (yy + colour) & 1;
         const int xx = 2 * kc + par;
-#if ACMMP_TILE_SKEW
-        tile[r * kTileP + kk + par] = texel(img, pitch, W, H, xx, yy);
-#else
         tile[e] = texel(img, pitch, W, H, xx, yy);
-#endif
     }
 }
 
@@ -411,25 +340,13 @@ DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour
 // The source side of the NCC runs on PAIRS of patch columns (2p, 2p+1) held
 // as packed-FP32 lanes (SoA): one v_pk_* instruction does the same IEEE
 // operation for both samples of a pair, and the pair's weights come from LDS
-// as one float4 (w_a, w_b, w_a*ref_a, w_b*ref_b), so no register shuffling is
-// needed to feed the packed ops. LDS slot of (column pair p, patch row jj):
-// jj * 3 + p, in the order the row loop reads them.
+// as one float2 (w_a, w_b), the reference pair from the tile, so no register
+// shuffling is needed to feed the packed ops. LDS slot of (column pair p,
+// patch row jj): jj * 3 + p, in the order the row loop reads them.
 constexpr int kPairs = kTaps / 2;
 constexpr int kSlots = kPairs * kTaps;
 DEV int wslot(int p, int jj) { return jj * kPairs + p; }
-
-// ACMMP_LDS_WR=1: slots hold (w_a, w_b, w_a*ref_a, w_b*ref_b) as float4
-// (72 KB per block, one ds_read_b128 per pair and no w*ref product in the
-// sample loop); 0: (w_a, w_b) float2 with the reference pair read from the
-// tile (36 KB per block).
-#ifndef ACMMP_LDS_WR
-#define ACMMP_LDS_WR 0
-#endif
-#if ACMMP_LDS_WR
-typedef float4 WSlot;
-#else
 typedef float2 WSlot;
-#endif
 
 struct PixPatch {
     WSlot *w;        // LDS: slot k of this lane at [k * kThreads]
@@ -455,18 +372,14 @@ DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, 
 // tb = tile index of sample (ii=0, jj=0) of this lane: ty*kTileW + tx + s
 DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatch &pp) {
     const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
-#if ACMMP_TILE_SKEW
-    const float center = tile[tb + 5 * kTileP + 2 + s];
-#else
     const float center = tile[tb - s + 5 * kTileW + 3];
-#endif
     float sum_ref = 0.0f, sum_rr = 0.0f, bw = 0.0f;
 #pragma unroll
     for (int ii = 0; ii < kTaps; ++ii) {
         float r_ref = 0.0f, r_rr = 0.0f, r_w = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
-            const float r = tile[tb + ii + 2 * kTileP * jj];
+            const float r = tile[tb + ii + 2 * kTileW * jj];
             const float w = bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
             const float wr = w * r;
             r_ref = dm_fma(w, r, r_ref);  // nvcc's contraction of `sum += w * r` (pin P3)
@@ -474,9 +387,6 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
             r_w += w;
             float *slot = reinterpret_cast<float *>(&pp.w[wslot(ii >> 1, jj) * kThreads]);
             slot[ii & 1] = w;
-#if ACMMP_LDS_WR
-            slot[2 + (ii & 1)] = wr;
-#endif
         }
         sum_ref += r_ref;
         sum_rr += r_rr;
@@ -508,12 +418,6 @@ __device__ u32x2 amdgcn_struct_buffer_load_b64(__amdgpu_buffer_rsrc_t rsrc, int 
                                                int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
 __device__ unsigned amdgcn_struct_buffer_load_b32(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                   int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
-
-// u8 quad (t00, t01, t10, t11) -> the fp32 texels, exactly (v_cvt_f32_ubyte0..3)
-DEV u32x4 unpack_quad(unsigned q) {
-    return u32x4{__float_as_uint((float)(q & 0xffu)), __float_as_uint((float)((q >> 8) & 0xffu)),
-                 __float_as_uint((float)((q >> 16) & 0xffu)), __float_as_uint((float)(q >> 24))};
-}
 
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 DEV f2v splat(float v) { return f2v{v, v}; }
@@ -601,13 +505,8 @@ DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v 
             rf.hq[2 * p] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ia, 0, 0, 0);
             rf.hq[2 * p + 1] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ib, 0, 0, 0);
         } else if (U8) {
-#ifdef ACMMP_DIAG_NOGATHER  // timing experiment only: no memory access
-            rf.q[2 * p] = ia * 0x01010101u;
-            rf.q[2 * p + 1] = ib * 0x01010101u;
-#else
             rf.q[2 * p] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ia, 0, 0, 0);
             rf.q[2 * p + 1] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ib, 0, 0, 0);
-#endif
         } else {
             rf.t[2 * p] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ia, 0, 0, 0);
             rf.t[2 * p + 1] = amdgcn_struct_buffer_load_b128(im.rsrc, (int)ib, 0, 0, 0);
@@ -639,7 +538,6 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
                                __builtin_fmaf(rf.ax[p].y, (float)db.y, (float)tb.y)};
             sv = fma2(rf.ay[p], r1 - r0, r0);
         } else if (U8) {
-#if ACMMP_PACKED_LERP
             // lerp_sample's operations with the pair's two samples in the two
             // components (sample a in .x, b in .y, as ax / ay already are):
             // top = fma(ax, t10 - t00, t00), bot = fma(ax, t11 - t01, t01),
@@ -652,31 +550,16 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
             const f2v top = fma2(rf.ax[p], t10 - t00, t00);
             const f2v bot = fma2(rf.ax[p], t11 - t01, t01);
             sv = fma2(rf.ay[p], bot - top, top);
-#else
-            sv = f2v{lerp_sample(unpack_quad(rf.q[2 * p]), rf.ax[p].x, rf.ay[p].x),
-                     lerp_sample(unpack_quad(rf.q[2 * p + 1]), rf.ax[p].y, rf.ay[p].y)};
-#endif
         } else {
             sv = f2v{lerp_sample(rf.t[2 * p], rf.ax[p].x, rf.ay[p].x),
                      lerp_sample(rf.t[2 * p + 1], rf.ax[p].y, rf.ay[p].y)};
         }
         // w from the weight slots, ref from the tile: w * ref is the same
         // IEEE product pixel_patch formed, so re-forming it is exact
-#ifdef ACMMP_DIAG_NOLDS  // timing experiment only: no LDS reads in the sample loop
-        const float2 w = make_float2(rf.ax[p].x, rf.ay[p].y);
-        const float rr[2] = {rf.ax[p].y, rf.ay[p].x};
-#else
         const WSlot w = wl[wslot(p, jj) * wstride];
-#if !ACMMP_LDS_WR
-        const float *rr = rt + 2 * kTileP * jj + 2 * p;
-#endif
-#endif
+        const float *rr = rt + 2 * kTileW * jj + 2 * p;
         const f2v wv = f2v{w.x, w.y};
-#if ACMMP_LDS_WR && !defined(ACMMP_DIAG_NOLDS)
-        const f2v wr = f2v{w.z, w.w};
-#else
         const f2v wr = wv * f2v{rr[0], rr[1]};
-#endif
         const f2v ws = wv * sv;
         acc_s[p] = fma2(wv, sv, acc_s[p]);  // `sum += w * s` contracted (pin P3)
         acc_ss[p] = fma2(ws, sv, acc_ss[p]);
@@ -711,23 +594,6 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
     f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
-#if ACMMP_PIPE_ROWS == 2
-    // two rows in flight ahead of the one being reduced (three rotating
-    // fetch buffers, the six rows straight-line)
-    RowFetch<TX> ra, rb, rc;
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 1, rb);
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 2, rc);
-    reduce_row<TX>(ra, wl, rt, wstride, 0, acc_s, acc_ss, acc_rs);
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 3, ra);
-    reduce_row<TX>(rb, wl, rt, wstride, 1, acc_s, acc_ss, acc_rs);
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 4, rb);
-    reduce_row<TX>(rc, wl, rt, wstride, 2, acc_s, acc_ss, acc_rs);
-    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 5, rc);
-    reduce_row<TX>(ra, wl, rt, wstride, 3, acc_s, acc_ss, acc_rs);
-    reduce_row<TX>(rb, wl, rt, wstride, 4, acc_s, acc_ss, acc_rs);
-    reduce_row<TX>(rc, wl, rt, wstride, 5, acc_s, acc_ss, acc_rs);
-#elif ACMMP_PIPE_ROWS
     // two rows per trip (ping-pong fetch buffers, no register copies)
     RowFetch<TX> ra, rb;
     fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
@@ -738,16 +604,6 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
         if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 2, ra);
         reduce_row<TX>(rb, wl, rt, wstride, jj + 1, acc_s, acc_ss, acc_rs);
     }
-#else
-    // rows are a rolled loop: one row's 6 gathers in flight, reduced, next row
-    // (unrolling lets the compiler hoist every row's address math and spill)
-#pragma unroll 1
-    for (int jj = 0; jj < kTaps; ++jj) {
-        RowFetch<TX> rf;
-        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj, rf);
-        reduce_row<TX>(rf, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
-    }
-#endif
     sum_src = 0.0f;
     sum_ss = 0.0f;
     sum_rs = 0.0f;
@@ -776,19 +632,6 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
-// ------------------------------------------------- diagnostic phase stamps
-// ACMMP_DIAG_STAMPS builds only (never the product library): per-phase
-// s_memtime cycle sums of the sweep kernel, accumulated by lane 0 of each wave.
-#ifdef ACMMP_DIAG_STAMPS
-__device__ unsigned long long g_diag_cycles[24];
-#define DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
-#define DIAG_ADD(slot, a, b) \
-    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[slot], (b) - (a)); } while (0)
-#else
-#define DIAG_T(var)
-#define DIAG_ADD(slot, a, b)
-#endif
-
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
 // wave-uniform). Reference samples come from the LDS tile, source samples
 // through ncc_sums.
@@ -806,7 +649,6 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float2 pt = project(H, (float)px, (float)py);
     if (pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f) return cost_max;
     float sum_src, sum_ss, sum_rs;
-#if ACMMP_FAST_RCP
     // hz is affine in the sample position, so its values over the patch lie
     // between the four corner values (up to rounding: the window test uses a
     // 2x margin). Inside the window the Newton reciprocal is bit-identical to
@@ -819,41 +661,8 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-#ifdef ACMMP_DIAG_STAMPS
-    {  // coherence census: the wave's bounding box of footprint records over
-       // the active lanes' patches (corner projections, +1 record margin);
-       // slot 13/14/15 += active lanes whose wave box fits 512 / 2048 / 8192
-       // records, slot 16 += all active lanes (0 when the window test fails)
-        float bx0 = 1e30f, bx1 = -1e30f, by0 = 1e30f, by1 = -1e30f;
-        const float cxs[2] = {xl, xr}, cys[2] = {yt, yb};
-        for (int a = 0; a < 2; ++a)
-            for (int b = 0; b < 2; ++b) {
-                const float2 q = project(H, cxs[a], cys[b]);
-                const float qx = fminf(fmaxf(q.x, -1.0f), (float)im.W), qy = fminf(fmaxf(q.y, -1.0f), (float)im.H);
-                bx0 = fminf(bx0, floorf(qx)); bx1 = fmaxf(bx1, floorf(qx));
-                by0 = fminf(by0, floorf(qy)); by1 = fmaxf(by1, floorf(qy));
-            }
-        const unsigned ux0 = (unsigned)(bx0 + 2.0f), ux1 = (unsigned)(bx1 + 2.0f);
-        const unsigned uy0 = (unsigned)(by0 + 2.0f), uy1 = (unsigned)(by1 + 2.0f);
-        const unsigned wx0 = __builtin_amdgcn_wave_reduce_min_u32(ux0, 1), wx1 = __builtin_amdgcn_wave_reduce_max_u32(ux1, 1);
-        const unsigned wy0 = __builtin_amdgcn_wave_reduce_min_u32(uy0, 1), wy1 = __builtin_amdgcn_wave_reduce_max_u32(uy1, 1);
-        const unsigned long long area = (unsigned long long)(wx1 - wx0 + 3) * (wy1 - wy0 + 3);
-        const unsigned long long act = __builtin_popcountll(__builtin_amdgcn_read_exec());
-        const bool first = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
-                           (unsigned)__builtin_ctzll(__builtin_amdgcn_read_exec());
-        if (first) {
-            if (fast && area <= 512) atomicAdd(&g_diag_cycles[13], act);
-            if (fast && area <= 2048) atomicAdd(&g_diag_cycles[14], act);
-            if (fast && area <= 8192) atomicAdd(&g_diag_cycles[15], act);
-            atomicAdd(&g_diag_cycles[16], act);
-        }
-    }
-#endif
     if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-#else
-    ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-#endif
     sum_src *= pp.inv_wsum;
     const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
     if (var_src < kMinVar) return cost_max;
@@ -1035,31 +844,21 @@ DEV BlockXY xcd_block() {
     return b;
 }
 
-// ACMMP_WAVE2D = R rows per wave (1, 2, 4 or 8): each wave covers 64/R columns
-// x R rows of the block instead of one 64-column row, so its gathers for
-// neighbouring patch rows overlap in the source image (L1 reuse within a
-// wave); the lane -> pixel map is all that changes.
+// kWaveRows = R rows per wave: each wave covers 64/R columns x R rows of the
+// block instead of one 64-column row, so its gathers for neighbouring patch
+// rows overlap in the source image (L1 reuse within a wave).
 DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     LaneGeom g;
-#if ACMMP_WAVE2D > 1
     // waves of C columns x R rows, kBX / C of them side by side per block row
-    constexpr int R = ACMMP_WAVE2D, C = 64 / R, WPR = kBX / C;
-    static_assert((ACMMP_WAVE2D == 2 || ACMMP_WAVE2D == 4 || ACMMP_WAVE2D == 8) && kBX % C == 0 && kBY % R == 0,
-                  "2D wave map");
+    constexpr int R = kWaveRows, C = 64 / R, WPR = kBX / C;
+    static_assert(kBX % C == 0 && kBY % R == 0, "2D wave map");
     const int w = tid >> 6, l = tid & 63;
     const int tx = (w % WPR) * C + (l % C), ty = (w / WPR) * R + l / C;
-#else
-    const int tx = tid % kBX, ty = tid / kBX;
-#endif
     g.k = b.bx * kBX + tx;
     g.py = b.by * kBY + ty;
     g.s = (g.py + colour) & 1;
     g.px = 2 * g.k + g.s;
-#if ACMMP_TILE_SKEW
-    g.tb = ty * kTileP + tx + 1;
-#else
     g.tb = ty * kTileW + tx + g.s;
-#endif
     return g;
 }
 
@@ -1070,7 +869,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, t
 // writes the colour-split "current" buffers. blockIdx.z = colour.
 template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
-    __shared__ float tile[kTileP * kTileH];
+    __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
@@ -1251,22 +1050,13 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
 // CheckerboardPropagation (src/ACMMP.cu:786-1173) for the pixels of one colour.
 // Neighbour state is read from the colour-split "current" buffers (the
 // half-sweep snapshot); own state lives in registers and is written to the
-// "next" buffer of this colour.
-//   MODE 0  the whole CheckerboardPropagation (k_sweep_f)
-//   MODE 1  split sweep, A: candidate search + phase A, results to KState::xcost /
-//           xprob / xdesc (k_sweep_a: no LDS candidate slots, fewer live VGPRs,
-//           ACMMP_SPLIT_A_WAVES waves per SIMD)
-//   MODE 2  split sweep, B: view selection, current cost, refinement, accept (k_sweep_b)
-template <int NS, int TX, int MODE>
+// "next" buffer of this colour. (A device function rather than the kernel
+// body: measured 4.15 -> 4.05 ms per launch)
+template <int NS, int TX>
 DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int iter) {
-    static_assert(MODE == 0 || (ACMMP_CAND_LDS && ACMMP_COMPACT_REFINE && ACMMP_SELECT_REGS),
-                  "the split sweep is built on the default variants");
-    __shared__ float tile[kTileP * kTileH];
+    __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
-#if ACMMP_CAND_LDS
     __shared__ float4 cand_lds[8 * kThreads];
-#endif
-    DIAG_T(t_start);
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block();
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
@@ -1286,14 +1076,11 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     float my_cost = cost_same[my];
     uint32_t my_sv = st.sv[colour][my];
     if (py >= kv.sweep_rows) {  // rows the reference grid never reaches
-        if (MODE != 1) {
-            st.plane_nx[colour][my] = my_plane;
-            st.cost_nx[colour][my] = my_cost;
-        }
+        st.plane_nx[colour][my] = my_plane;
+        st.cost_nx[colour][my] = my_cost;
         return;
     }
     const acmmp_params &prm = kv.prm;
-    const size_t xp = st.xplane;  // split sweep: one plane per slot of xcost / xprob / xdesc
     const acmmp_camera &c0 = kv.cam[0];
     const int nsrc = kv.nsrc;
     const int center = py * width + px;
@@ -1303,13 +1090,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     // index of direction d's winner; bit d of `same`: it is this colour.
     int cidx[8];
     uint32_t flags = 0, same = 0;
-    if (MODE == 2) {  // split sweep, B: the winners phase A found (same snapshot)
-#pragma unroll
-        for (int d = 0; d < 8; ++d) cidx[d] = (int)st.xdesc[(size_t)d * xp + my];
-        const uint32_t fs = st.xdesc[(size_t)8 * xp + my];
-        flags = fs & 0xffu;
-        same = fs >> 8;
-    } else {
     float costMin;
     if (py > 2) {  // up_far (opposite colour)
         flags |= 1u << 1;
@@ -1442,60 +1222,25 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         same |= (uint32_t)bs << 6;
     }
 #undef CS
-    if (MODE == 1) {  // split sweep, A: the winners for phase B
-#pragma unroll
-        for (int d = 0; d < 8; ++d) st.xdesc[(size_t)d * xp + my] = (uint32_t)cidx[d];
-        st.xdesc[(size_t)8 * xp + my] = flags | same << 8;
-    }
-    }  // search
-#if ACMMP_CAND_LDS
     // the 8 winners' planes, fetched once into this lane's LDS slots (the
     // NCC prologues then read them at LDS latency, not L2's)
-    // (split sweep, A: no LDS slots, so more blocks fit; the planes come from
-    // L1/L2 by the same select chain as without ACMMP_CAND_LDS)
     float4 *cand_slot = cand_lds + threadIdx.y * kBX + threadIdx.x;
-    if (MODE != 1) {
 #pragma unroll
-        for (int d = 0; d < 8; ++d)
-            if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
-    }
-    auto cand = [&](int d) -> float4 {
-        if constexpr (MODE == 1) {
-            int ci = cidx[0];
-#pragma unroll
-            for (int e = 1; e < 8; ++e) ci = (d == e) ? cidx[e] : ci;
-            return (((same >> d) & 1u) ? plane_same : plane_opp)[ci];
-        } else {
-            return cand_slot[d * kThreads];
-        }
-    };
-    auto cand_dyn = cand;
-#else
-    auto cand = [&](int d) -> float4 { return (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]]; };
-    // wave-uniform d: select chain instead of a dynamically indexed (scratch) array
-    auto cand_dyn = [&](int d) -> float4 {
-        int ci = cidx[0];
-#pragma unroll
-        for (int e = 1; e < 8; ++e) ci = (d == e) ? cidx[e] : ci;
-        return (((same >> d) & 1u) ? plane_same : plane_opp)[ci];
-    };
-#endif
+    for (int d = 0; d < 8; ++d)
+        if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
+    auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
 
-    DIAG_T(t_search);
     PixPatch pp;
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
     pp.rt = tile + g.tb;
     pixel_patch(kv, tile, g.tb, g.s, pp);
-    DIAG_T(t_patch);
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
-    // (split sweep: xcost in HBM, A writes it, B reads the sampled views)
     float cost_array[8][NS];
     // view-selection inputs (:994-1032), folded into the view-major candidate
     // loop so each view's 8 costs are consumed from registers
     float probs[NS];
-    if (MODE != 2) {
     uint32_t nb[4];
     {
         const uint32_t *sv_opp = st.sv[oc];
@@ -1508,35 +1253,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
     // view-major: the 8 candidates of one source view gather from nearly the
     // same footprint, back to back (results are independent)
-#ifdef ACMMP_DIAG_STAMPS
-    {  // duplicate-candidate census: slot 5 = flagged candidates, 6 = equal to an
-       // earlier candidate, 7 = equal to the pixel's current plane
-        unsigned long long n = 0, dup = 0, cur = 0;
-        for (int d = 0; d < 8; ++d) {
-            if (!((flags >> d) & 1u)) continue;
-            const float4 a = cand(d);
-            ++n;
-            bool found = false;
-            for (int e = 0; e < d && !found; ++e)
-                if (((flags >> e) & 1u)) {
-                    const float4 b = cand(e);
-                    found = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
-                }
-            dup += found;
-            cur += (a.x == my_plane.x && a.y == my_plane.y && a.z == my_plane.z && a.w == my_plane.w);
-        }
-        atomicAdd(&g_diag_cycles[5], n);
-        atomicAdd(&g_diag_cycles[6], dup);
-        atomicAdd(&g_diag_cycles[7], cur);
-        // wave-level: max unique candidates over the wave (slot 12), lanes' sum
-        // (11), waves (10)
-        const int uniq = (int)(n - dup);
-        atomicAdd(&g_diag_cycles[11], (unsigned long long)uniq);
-        unsigned long long wmax = 0;
-        for (int u = 1; u <= 8; ++u) wmax += __ballot(uniq >= u) != 0;
-        if ((threadIdx.x & 63) == 0) { atomicAdd(&g_diag_cycles[12], wmax); atomicAdd(&g_diag_cycles[10], 1ull); }
-    }
-#endif
     for (int v = 0; v < nsrc; ++v) {
         // one NCC call site: the candidate loop stays rolled (d is wave-uniform,
         // the candidate's index is picked by selects), and the sampling
@@ -1547,10 +1263,9 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 #pragma unroll 1
         for (int d = 0; d < 8; ++d) {
             float c;
-            if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand_dyn(d));
+            if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
             else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
-            if (MODE == 1) st.xcost[(size_t)(d * nsrc + v) * xp + my] = c;
-            else cost_array[d][v] = c;
+            cost_array[d][v] = c;
             if (c < cost_threshold) {
                 tmpw += dm_expf(c * c / (-0.18f));
                 count++;
@@ -1563,15 +1278,10 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         float pr = 0.0f;
         if (count > 2 && count_false < 3) pr = tmpw / count;
         else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
-        if (MODE == 1) st.xprob[(size_t)v * xp + my] = pr * vsp;
-        else probs[v] = pr * vsp;
+        probs[v] = pr * vsp;
     }
-    if (MODE == 1) return;  // split sweep, A ends here
-    }  // phase A
 
-    DIAG_T(t_phaseA);
     // ---- multi-hypothesis joint view selection (:994-1056)
-#if ACMMP_SELECT_REGS
     // CDF in registers (static indices over NS, predicated on i < nsrc): the
     // 15 draws then need no dependent scratch loads. The CDF is
     // nondecreasing (non-negative terms; once NaN it stays NaN), so the
@@ -1583,7 +1293,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         float sum = 0.0f;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            cdf[i] = i < nsrc ? (MODE == 2 ? st.xprob[(size_t)i * xp + my] : probs[i]) : 0.0f;
+            cdf[i] = i < nsrc ? probs[i] : 0.0f;
             if (i < nsrc) sum += cdf[i];
         }
         const float inv = 1.0f / sum;
@@ -1608,44 +1318,13 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         for (int i = 1; i < NS; ++i) at = idx == i ? cdf[i] : at;
         if (idx < nsrc && at > rand_prob) vw.add(idx);
     }
-#else
-    {  // TransformPDFToCDF (:107-121)
-        float sum = 0.0f;
-        for (int i = 0; i < nsrc; ++i) sum += probs[i];
-        const float inv = 1.0f / sum;
-        float cum = 0.0f;
-        for (int i = 0; i < nsrc; ++i) {
-            cum += probs[i] * inv;
-            probs[i] = cum;
-        }
-    }
-    dm_rng rs = make_rng(kv, center, 1u + (uint32_t)iter);
-    ViewCounts vw;
-    for (int sample = 0; sample < 15; ++sample) {
-        const float rand_prob = dm_rng_uniform(&rs) - FLT_EPSILON;
-        for (int image_id = 0; image_id < nsrc; ++image_id) {
-            if (probs[image_id] > rand_prob) { vw.add(image_id); break; }
-        }
-    }
-#endif
     uint32_t temp_sv = 0;
     float weight_norm = 0;
     for (int i = 0; i < nsrc; ++i) {
         const int c = vw.get(i);
         if (c > 0) { temp_sv |= (1u << i); weight_norm += (float)c; }
     }
-
-#ifdef ACMMP_DIAG_STAMPS
-    {  // refinement divergence: views with a sampled weight per lane (9) vs the
-       // union over the wave (8)
-        unsigned long long uni = 0;
-        for (int v = 0; v < nsrc; ++v) uni += __ballot(vw.get(v) > 0) != 0;
-        atomicAdd(&g_diag_cycles[9], (unsigned long long)__builtin_popcount(temp_sv));
-        if ((threadIdx.x & 63) == 0) atomicAdd(&g_diag_cycles[8], uni);
-    }
-#endif
     float final_costs[8];
-#if ACMMP_SELECT_REGS
     if (!prm.geom_consistency) {
         // photometric: the NS cost loads of a candidate issued together
         // (static offsets), unsampled views add +0 (costs are finite and
@@ -1656,13 +1335,11 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             for (int j = 0; j < NS; ++j)
                 if (j < nsrc) {
                     const float wj = (float)vw.get(j);
-                    const float cj = MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j];
-                    fc += wj > 0 ? wj * cj : 0.0f;
+                    fc += wj > 0 ? wj * cost_array[i][j] : 0.0f;
                 }
             final_costs[i] = fc / weight_norm;
         }
     } else
-#endif
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
         const bool fl = (flags >> i) & 1u;
@@ -1672,11 +1349,11 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             const float wj = (float)vw.get(j);
             if (wj > 0) {
                 if (prm.geom_consistency) {
-                    const float cij = MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j];
+                    const float cij = cost_array[i][j];
                     if (fl) fc += wj * (cij + 0.2f * geom_cost(kv, j + 1, hi, px, py));
                     else fc += wj * (cij + 0.1f * 3.0f);
                 } else {
-                    fc += wj * (MODE == 2 ? st.xcost[(size_t)(i * nsrc + j) * xp + my] : cost_array[i][j]);
+                    fc += wj * cost_array[i][j];
                 }
             }
         }
@@ -1689,7 +1366,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             if (final_costs[i] <= m) { m = final_costs[i]; min_cost_idx = i; }
     }
 
-    DIAG_T(t_select);
     // ---- current hypothesis (:1080-1093) + refinement (:707-784): one NCC
     // site. t = 0 evaluates the current plane; t = 1..5 the refinement planes.
     const bool has_prior = prm.planar_prior && st.mask[center] > 0;
@@ -1716,31 +1392,19 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     const float beta = 0.18f;
 
     for (int t = 0; t < 6; ++t) {
-#if ACMMP_COMPACT_REFINE
         // all 5 refinement costs at once (their planes go to LDS slots 0..4)
         if (t == 1)
             refine_costs_compact<TX>(kv, tile, wlds, cand_lds, pp, vw, nsrc, colour, blk, ref_depth, ref_normal,
                                      px, py);
-#endif
         float4 h;
-        if (t == 0) {
-            h = my_plane;
-        } else {
-#if ACMMP_COMPACT_REFINE
-            h = cand_lds[(t - 1) * kThreads + pp.wo];  // stored by refine_costs_compact
-#else
-            h = ref_normal(t - 1);
-            h.w = distance_to_origin(c0, px, py, ref_depth(t - 1), h);
-#endif
-        }
+        if (t == 0) h = my_plane;
+        else h = cand_lds[(t - 1) * kThreads + pp.wo];  // stored by refine_costs_compact
         // views with a zero sampled weight contribute +0 in the reference
         // (weight 0 * finite cost), so their NCC is skipped: bit-identical
         float tc = 0.0f;
-#if ACMMP_COMPACT_REFINE
         if (t >= 1) {
             tc = cmp_res(cand_lds, t - 1, pp.wo);
         } else
-#endif
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
@@ -1874,28 +1538,12 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     st.plane_nx[colour][my] = my_plane;
     st.cost_nx[colour][my] = my_cost;
     st.sv[colour][my] = my_sv;
-    DIAG_T(t_end);
-    DIAG_ADD(0, t_start, t_search);
-    DIAG_ADD(1, t_search, t_patch);
-    DIAG_ADD(2, t_patch, t_phaseA);
-    DIAG_ADD(3, t_phaseA, t_select);
-    DIAG_ADD(4, t_select, t_end);
 }
 
 template <int NS, int TX>
-__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep_f(const KViews *__restrict__ kvp, KState st, int colour,
-                                                                    int iter) {
-    sweep_body<NS, TX, 0>(kvp, st, colour, iter);
-}
-template <int NS, int TX>
-__global__ __launch_bounds__(256, ACMMP_SPLIT_A_WAVES) void k_sweep_a(const KViews *__restrict__ kvp, KState st,
-                                                                      int colour, int iter) {
-    sweep_body<NS, TX, 1>(kvp, st, colour, iter);
-}
-template <int NS, int TX>
-__global__ __launch_bounds__(256, ACMMP_SWEEP_WAVES) void k_sweep_b(const KViews *__restrict__ kvp, KState st, int colour,
-                                                                    int iter) {
-    sweep_body<NS, TX, 2>(kvp, st, colour, iter);
+__global__ __launch_bounds__(256, kSweepWaves) void k_sweep_f(const KViews *__restrict__ kvp, KState st, int colour,
+                                                              int iter) {
+    sweep_body<NS, TX>(kvp, st, colour, iter);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
@@ -1970,7 +1618,7 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
 template <int NS, int TX>
 __global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
-    __shared__ float tile[kTileP * kTileH];
+    __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
@@ -2087,19 +1735,6 @@ hipError_t launch_pad_quad(const float *src, int spitch, int W, int H, uint32_t 
     dim3 block(64, 4), grid((W + 2 + 63) / 64, (H + 2 + 3) / 4);
     k_pad_quad<<<grid, block, 0, s>>>(src, spitch, W, H, dst, dpitch, not_u8);
     return hipGetLastError();
-}
-
-int diag_read_cycles(unsigned long long *out8) {
-#ifdef ACMMP_DIAG_STAMPS
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_cycles), 24 * sizeof(unsigned long long)) != hipSuccess)
-        return -3;
-    unsigned long long z[24] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_cycles), z, sizeof(z)) != hipSuccess) return -3;
-    return 0;
-#else
-    (void)out8;
-    return -5;
-#endif
 }
 
 // Exhaustive check of recip_newton against IEEE 1/z over every float32 bit
@@ -2235,12 +1870,7 @@ hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st,
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
-    if constexpr (kSplitSweep) {  // phase A (more waves per SIMD), then selection + refinement
-        ACMMP_LAUNCH_NS(k_sweep_a, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
-        ACMMP_LAUNCH_NS(k_sweep_b, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
-    } else {
-        ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
-    }
+    ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
     return hipGetLastError();
 }
 

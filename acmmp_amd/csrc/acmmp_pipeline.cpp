@@ -210,13 +210,12 @@ int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
     return write_png8(path, W, H, 3, rgb.data());
 }
 
-// Runs fn(0..n-1) on up to 16 host threads. Returns the status of the lowest
+// Runs fn(0..n-1) on acmmp_host_threads() threads. Returns the status of the lowest
 // failing index and leaves its message in this thread's error slot, so the
 // caller sees what the sequential loop would have reported first.
 template <class Fn>
 int parallel_views(int n, Fn fn) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int workers = std::min<int>(n, (int)std::min(hw, 16u));
+    const int workers = std::min<int>(n, acmmp_host_threads());
     std::vector<int> rc((size_t)n, ACMMP_OK);
     std::vector<std::string> msg((size_t)n);
     std::atomic<int> next{0};

@@ -457,7 +457,7 @@ class Driver {
             }
         };
         std::vector<std::thread> pool;
-        const int nt = (int)std::min<size_t>(16, need.size());
+        const int nt = (int)std::min<size_t>((size_t)acmmp_host_threads(), need.size());
         for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
         for (auto &t : pool) t.join();
         for (size_t k = 0; k < need.size(); ++k)

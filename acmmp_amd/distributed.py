@@ -292,7 +292,7 @@ class ViewParallelPipeline:
 
         from concurrent.futures import ThreadPoolExecutor
         order = sorted(need)
-        with ThreadPoolExecutor(max_workers=max(1, min(16, len(order)))) as ex:
+        with ThreadPoolExecutor(max_workers=max(1, min(lib.acmmp_host_threads(), len(order)))) as ex:
             loaded = list(ex.map(load, order))  # re-raises the first failure in id order
         for i, (img, cam) in zip(order, loaded):
             self.images[i] = torch.from_numpy(img).to(self.tdev)

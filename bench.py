@@ -218,7 +218,11 @@ def main():
         "data": "synthetic (seeded analytic scene rendered into HBM; no DTU data offline)",
         "config": {
             "workload": f"cfg2: {args.views} ref views/GPU at {W}x{H}, {n_img} images/problem, "
-                        f"{args.iters} iters, photometric + RCCL depth all-gather + geometric pass",
+                        f"{args.iters} iters, photometric + "
+                        + (f"{'RCCL' if backend == 'nccl' else 'gloo'} depth all-gather + " if distributed else "")
+                        + "geometric pass",
+            "geom_iters_note": f"the geometric pass runs {args.iters} iterations as BASELINE cfg2 states; the "
+                               "reference's SetGeomConsistencyParams forces 2 (src/ACMMP.cpp:447-454)",
             "views_per_gpu": args.views,
             "width": W,
             "height": H,
@@ -320,7 +324,11 @@ def cpu_baseline(args, setup, images, cams, srcs, mine, all_depth, gpu_value):
     from acmmp_amd import ACMMP, default_params, scene
     from acmmp_amd._abi import Camera
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    from acmmp_amd import load_library
+    # every host thread this process may use: the smallest of the affinity
+    # mask, the cgroup CPU quota and OMP_NUM_THREADS, the launcher's declared
+    # budget (the library's own pools use the same count)
+    threads = int(load_library().acmmp_host_threads())
     model, ncpu, avail = host_cpu()
     oracle.build()
 
@@ -385,7 +393,17 @@ def cpu_baseline(args, setup, images, cams, srcs, mine, all_depth, gpu_value):
         "cpu_model": model,
         "nproc": ncpu,
         "cpus_available": avail,
+        "cores_note": (f"cores = the {threads} host threads this process is granted (affinity mask, cgroup "
+                       f"quota and OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}: a shared GPU "
+                       f"box gives one GPU's process a {threads}-CPU share of its {avail} threads); on an "
+                       "unshared host the oracle uses every core" if threads < avail else
+                       "cores = every host thread available to the process"),
+        "value_per_core": round(cpu_value / threads, 6),
+        "all_core_estimate": round(cpu_value / threads * avail, 4),
+        "all_core_estimate_note": f"value_per_core x {avail} available threads: linear OpenMP scaling, an upper "
+                                  "bound for the CPU (the pixel loop is embarrassingly parallel per colour)",
         "speedup_gpu_vs_cpu": round(gpu_value / cpu_value, 1),
+        "speedup_gpu_vs_all_core_estimate": round(gpu_value / (cpu_value / threads * avail), 1),
         "cfg1": {
             "workload": "5 views 400x300, 3 iters, photometric (BASELINE configs[0]), in full",
             "cpu_s": round(t1, 3),

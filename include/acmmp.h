@@ -332,6 +332,12 @@ int acmmp_get_texel_bits(const acmmp_ctx *ctx);
 int acmmp_device_count(void);
 /* Library build string (arch, flags). */
 const char *acmmp_version(void);
+/* Host threads the library's thread pools use (image decodes, fusion, the
+ * view-parallel driver's loads): the smallest of the affinity mask, the
+ * cgroup CPU quota and OMP_NUM_THREADS (the launcher's declared budget);
+ * ACMMP_HOST_THREADS overrides. The reference is single-threaded apart from
+ * the OpenMP PLY writer (src/ACMMP.cpp:405). */
+int acmmp_host_threads(void);
 
 /* ---- Pass driver: the reference's pipeline around RunPatchMatch
  *      (src/acmmp_definitions.cpp:179-403, src/ACMMP.cpp:525-809), reading

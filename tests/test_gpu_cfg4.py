@@ -1,0 +1,141 @@
+"""cfg4 (BASELINE.json configs[3]) at its real problem shape:
+every view with its 20 best sources (N = 21, colmap2mvsnet_acm.py:415), two
+scales with JBU + hierarchy + planar prior, two geometric passes per scale
+(src/main_ACMMP.cpp:96-176), view-parallel.
+
+(a) 22 views at 1010x760 (ComputeMultiScaleSettings: 505x380 -> 1010x760)
+    through BOTH view-parallel drivers at world 2 (two ranks sharing the
+    box's GPU: gloo for the Python driver, TCP for acmmp_main), every output
+    map bit-identical to OraclePipeline.run_multi_scale("jacobi"). The oracle
+    takes hours on this shape, so its maps are pinned by SHA-256 digests made
+    once by tools/gen_cfg4_golden.py (tests/golden/cfg4_ms_n21.json), together
+    with the digests of the input files the test rebuilds.
+(b) the full cfg4 shape, 49 views at 1600x1200 (800x600 -> 1600x1200), through
+    both drivers at world 1 (RCCL in acmmp_main): every .dmb bit-identical
+    between the two drivers, and the maps physically right — finite depths
+    inside the depth range, costs in [0, 2] or NaN, and the final geometric
+    depths within 1 % (median relative error) of the scene's analytic depth
+    on confident pixels.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from acmmp_amd import io as aio
+from acmmp_amd import scene
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import gen_cfg4_golden as golden  # noqa: E402
+from test_gpu_distributed import _spawn  # noqa: E402
+from test_gpu_vp_cli import _launch  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "cfg4_ms_n21.json")
+
+
+def _digests(out_folder, names):
+    got = {}
+    for key in names:
+        view, name = key.split("/")
+        path = os.path.join(aio.result_folder(out_folder, int(view)), name + ".dmb")
+        got[key] = golden.map_digest(aio.read_dmb(path))
+    return got
+
+
+@pytest.fixture(scope="module")
+def ms_n21(tmp_path_factory):
+    with open(GOLDEN) as f:
+        ref = json.load(f)
+    d = str(tmp_path_factory.mktemp("cfg4_ms_n21"))
+    golden.make_dense(d)
+    inputs = golden.file_digests(d)
+    bad = sorted(k for k in ref["inputs"] if inputs.get(k) != ref["inputs"][k])
+    assert not bad, f"rebuilt inputs differ from the fixture generator's: {bad[:5]}"
+    return d, ref["maps"]
+
+
+def _check(out_folder, maps):
+    got = _digests(out_folder, maps)
+    bad = sorted(k for k in maps if got[k] != maps[k])
+    assert not bad, f"{len(bad)} / {len(maps)} maps differ from the oracle's: {bad[:8]}"
+
+
+@pytest.mark.timeout(900)
+def test_multi_scale_n21_python_driver_world2(ms_n21):
+    d, maps = ms_n21
+    mine = _spawn(2, d, "gloo", "/C4PY")
+    assert sorted(mine[0] + mine[1]) == list(range(golden.NUM_VIEWS))
+    _check(d + "/C4PY", maps)
+
+
+@pytest.mark.timeout(900)
+def test_multi_scale_n21_cpp_driver_world2(ms_n21):
+    d, maps = ms_n21
+    _launch(d, "/C4CPP", 2, "tcp", ["--no_fusion"], timeout=800)
+    _check(d + "/C4CPP", maps)
+
+
+# ---------------------------------------------------------------- (b)
+FULL_VIEWS, FULL_W, FULL_H = 49, 1600, 1200
+
+
+@pytest.fixture(scope="module")
+def full_cfg4(tmp_path_factory):
+    """49 views at 1600x1200 rendered on the GPU (render_torch, with the
+    analytic depth), written as a COLMAP-converted dense folder."""
+    import torch
+    from PIL import Image
+    d = str(tmp_path_factory.mktemp("cfg4_full"))
+    os.makedirs(os.path.join(d, "images"))
+    os.makedirs(os.path.join(d, "cams"))
+    setup = scene.scene_setup(num_views=FULL_VIEWS, width=FULL_W, height=FULL_H)
+    dev = torch.device("cuda", 0)
+    truth = {}
+    for i in range(FULL_VIEWS):
+        img, dep = scene.render_torch(setup, i, dev, with_depth=True)
+        Image.fromarray(img.cpu().numpy().astype(np.uint8), "L").save(
+            os.path.join(d, "images", "%08d.jpg" % i), "JPEG", quality=95)
+        truth[i] = dep.cpu().numpy()
+        R, t, _, _ = setup.poses[i]
+        aio.write_camera(os.path.join(d, "cams", "%08d_cam.txt" % i), setup.K, R, t, *scene.DEPTH_LINE)
+    sel = []
+    for i in range(FULL_VIEWS):
+        srcs = setup.pairs[i][:20]
+        sel.append([(s, len(srcs) - k) for k, s in enumerate(srcs)])
+    aio.write_pair(os.path.join(d, "pair.txt"), sel)
+    torch.cuda.synchronize()
+    return d, truth
+
+
+@pytest.mark.timeout(1200)
+def test_full_cfg4_drivers_agree_and_match_geometry(full_cfg4):
+    from acmmp_amd.distributed import ViewParallelPipeline
+    d, truth = full_cfg4
+    ViewParallelPipeline(d, "/F4PY", device=0).run()
+    _launch(d, "/F4CPP", 1, "rccl", ["--no_fusion"], timeout=1000)
+    names = ("depths", "depths_geom", "normals", "costs")
+    errs = []
+    for v in range(FULL_VIEWS):
+        for name in names:
+            a = aio.read_dmb(os.path.join(aio.result_folder(d + "/F4PY", v), name + ".dmb"))
+            b = aio.read_dmb(os.path.join(aio.result_folder(d + "/F4CPP", v), name + ".dmb"))
+            assert golden.map_digest(a) == golden.map_digest(b), f"view {v} {name}: the drivers differ"
+        depth = aio.read_dmb(os.path.join(aio.result_folder(d + "/F4PY", v), "depths_geom.dmb"))
+        cost = aio.read_dmb(os.path.join(aio.result_folder(d + "/F4PY", v), "costs.dmb"))
+        assert depth.shape == (FULL_H, FULL_W)
+        assert np.isfinite(depth).all(), f"view {v}: non-finite depth"
+        ok = np.isnan(cost) | ((cost >= 0) & (cost <= 2))
+        assert ok.all(), f"view {v}: costs outside [0, 2] u NaN"
+        gt = truth[v]
+        conf = (gt > 0) & np.isfinite(cost) & (cost < 0.3)
+        assert conf.mean() > 0.3, f"view {v}: only {conf.mean():.1%} confident pixels"
+        rel = np.abs(depth[conf] - gt[conf]) / gt[conf]
+        errs.append(float(np.median(rel)))
+    assert max(errs) < 0.01, f"median relative depth error per view up to {max(errs):.4f}"

@@ -56,19 +56,6 @@ def test_every_texel_form_matches_oracle(prob, monkeypatch, form, bits):
     _check(prm, cams, imgs, pl, co, sv, f"{bits}-bit texels")
 
 
-@pytest.mark.parametrize("form,bits", [("u8", 8), ("h16", 16)])
-@pytest.mark.parametrize("skew", [1, 5, 16])
-def test_skewed_record_rows_match_oracle(prob, monkeypatch, form, bits, skew):
-    """ACMMP_PAD_SKEW offsets the compact forms' row pitch by whole records
-    (rows no longer start on a 128-B line): a layout change only."""
-    cams, imgs = prob
-    monkeypatch.setenv("ACMMP_TEXEL", form)
-    monkeypatch.setenv("ACMMP_PAD_SKEW", str(skew))
-    got, prm, pl, co, sv = _run(cams, imgs)
-    assert got == bits
-    _check(prm, cams, imgs, pl, co, sv, f"{bits}-bit texels, row skew {skew}")
-
-
 def test_texel_f32_switch(prob, monkeypatch):
     cams, imgs = prob
     monkeypatch.setenv("ACMMP_TEXEL_F32", "1")
@@ -129,28 +116,34 @@ def test_quads_at_image_borders(monkeypatch, form, bits):
     _check(prm, cams, imgs, pl, co, sv, f"{form} borders")
 
 
-@pytest.mark.parametrize("mixed", [False, True])
+@pytest.mark.parametrize("mixed", [None, "h16", "f32"])
 def test_textures_match_oracle(prob, mixed):
     """acmmp_texture_create + acmmp_set_images_textures (records built once,
     borrowed by the engine: the drivers' and bench's path). mixed: one view
-    holds fractional texels, so its texture is fp32 while the others are u8
-    quads; the engine then re-pads the problem in the common (fp32) form."""
+    holds fractional texels, so its texture falls back from u8 quads to f16
+    difference quads (quarter steps, exact in f16: the texture's records are
+    re-sized for the second form it tries) or to fp32 (thirds), while the
+    others are u8 quads; the engine then re-pads the problem in the common
+    form (the least compact)."""
     import torch
     from acmmp_amd.engine import Texture
     cams, imgs = prob
     imgs = [np.asarray(im, np.float32).copy() for im in imgs]
-    if mixed:
-        imgs[3] = imgs[3] + 0.1  # not exact in f16 either: the fp32 form
+    if mixed == "h16":
+        imgs[3] = imgs[3] + 0.25
+    elif mixed == "f32":
+        imgs[3] = imgs[3] + np.float32(1.0 / 3.0)
+    odd = {None: 8, "h16": 16, "f32": 32}[mixed]
     dev = torch.device("cuda", 0)
     timgs = [torch.from_numpy(im).to(dev) for im in imgs]
     torch.cuda.synchronize()
     tex = [Texture.of(t, 0) for t in timgs]
-    assert [t.bits for t in tex] == [32 if (mixed and i == 3) else 8 for i in range(len(tex))]
+    assert [t.bits for t in tex] == [odd if i == 3 else 8 for i in range(len(tex))]
     with ACMMP(0) as eng:
         eng.set_params(_params(2))
         eng.set_images_textures(cams, tex)
-        assert eng.texel_bits() == (32 if mixed else 8)
+        assert eng.texel_bits() == (32 if mixed == "f32" else 16 if mixed else 8)
         prm = eng.params
         eng.RunPatchMatch()
         pl, co, sv = eng.plane_hypotheses(), eng.costs(), eng.selected_views()
-    _check(prm, cams, imgs, pl, co, sv, "textures, mixed" if mixed else "textures")
+    _check(prm, cams, imgs, pl, co, sv, f"textures, {mixed or 'u8'}")
