@@ -5,8 +5,11 @@
 //    a baseline (SOF0/SOF1, 8-bit, Huffman) JPEG decoder that returns the
 //    luminance plane exactly as libjpeg's JCS_GRAYSCALE output does — the
 //    ISLOW integer IDCT with its range-limit table, Y taken without colour
-//    conversion. Progressive / arithmetic / 12-bit files are rejected
-//    (ACMMP_ERR_UNSUPPORTED).
+//    conversion; and progressive (SOF2) files, whose spectral-selection /
+//    successive-approximation scans rebuild the same coefficients libjpeg's
+//    jdphuff.c does before the same IDCT (camera JPEGs reach the loader
+//    unchanged: colmap2mvsnet_acm.py:453-454). Arithmetic-coded / lossless /
+//    12-bit files are rejected (ACMMP_ERR_UNSUPPORTED).
 //    The IDCT algorithm and its constants (the Loeffler-Ligtenberg-Moschytz
 //    factorisation as laid out in jidctint.c) are the Independent JPEG
 //    Group's; this file re-implements them, it contains no IJG source.
@@ -74,6 +77,8 @@ struct Jpeg {
     Huff dc[4], ac[4];
     int restart = 0;
     bool sof = false;
+    bool progressive = false;  // SOF2
+    int eobrun = 0;            // progressive AC scans: blocks left in the current end-of-band run
     // bit reader
     uint32_t bitbuf = 0;
     int bitcnt = 0;
@@ -214,7 +219,10 @@ void handle_restart(Jpeg &j) {
     while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] >= 0xD0 && j.p[1] <= 0xD7)) ++j.p;
     if (j.p + 1 < j.end) j.p += 2;
     for (int c = 0; c < j.ncomp; ++c) j.comp[c].pred = 0;
+    j.eobrun = 0;
 }
+
+bool decode_scan_progressive(Jpeg &j, const int *sc, int ns, int ss, int se, int ah, int al);
 
 bool decode_scan(Jpeg &j, const uint8_t *hdr, int len) {
     const int ns = hdr[0];
@@ -228,12 +236,13 @@ bool decode_scan(Jpeg &j, const uint8_t *hdr, int len) {
         if (sc[i] < 0) return false;
         j.comp[sc[i]].td = tbl >> 4;
         j.comp[sc[i]].ta = tbl & 15;
-        if (j.comp[sc[i]].td > 3 || j.comp[sc[i]].ta > 3 || !j.dc[j.comp[sc[i]].td].present ||
-            !j.ac[j.comp[sc[i]].ta].present)
-            return false;
+        if (j.comp[sc[i]].td > 3 || j.comp[sc[i]].ta > 3) return false;
+        // (a progressive scan needs only the table of its kind: checked there)
+        if (!j.progressive && (!j.dc[j.comp[sc[i]].td].present || !j.ac[j.comp[sc[i]].ta].present)) return false;
     }
     const int ss = hdr[1 + 2 * ns], se = hdr[2 + 2 * ns], ahal = hdr[3 + 2 * ns];
-    if (ss != 0 || se != 63 || ahal != 0) return false;  // sequential only
+    if (j.progressive) return decode_scan_progressive(j, sc, ns, ss, se, ahal >> 4, ahal & 15);
+    if (ss != 0 || se != 63 || ahal != 0) return false;  // sequential
     for (int i = 0; i < ns; ++i) j.comp[sc[i]].pred = 0;
     j.bitbuf = 0;
     j.bitcnt = 0;
@@ -271,6 +280,167 @@ bool decode_scan(Jpeg &j, const uint8_t *hdr, int len) {
         }
     }
     // continue after the entropy-coded segment
+    while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] != 0x00 && !(j.p[1] >= 0xD0 && j.p[1] <= 0xD7))) ++j.p;
+    return true;
+}
+
+// ---- progressive scans (ITU T.81 G.1.2; the decoding of libjpeg's
+// jdphuff.c, re-implemented): DC first / DC refinement scans (possibly
+// interleaved) and single-component AC first / AC refinement scans over a
+// spectral band [ss, se] at bit position al. Coefficients accumulate in the
+// component's coefficient array (natural order); dst == nullptr decodes a
+// component whose coefficients are not kept (bits consumed all the same).
+void prog_dc_first(Jpeg &j, Comp &c, int16_t *dst, int al) {
+    const int t = decode_huff(j, j.dc[c.td]);
+    if (t > 16) {
+        j.err = ACMMP_ERR_IO;
+        return;
+    }
+    c.pred += extend(getbits(j, t), t);
+    if (dst) dst[0] = (int16_t)(int)((uint32_t)c.pred << al);
+}
+
+void prog_dc_refine(Jpeg &j, int16_t *dst, int al) {
+    if (getbits(j, 1) && dst) dst[0] = (int16_t)(dst[0] | (1 << al));
+}
+
+void prog_ac_first(Jpeg &j, const Comp &c, int16_t *dst, int ss, int se, int al) {
+    if (j.eobrun > 0) {
+        --j.eobrun;
+        return;
+    }
+    for (int k = ss; k <= se; ++k) {
+        const int rs = decode_huff(j, j.ac[c.ta]);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz) {
+            k += r;
+            const int v = extend(getbits(j, sz), sz);
+            if (k > 63) {
+                j.err = ACMMP_ERR_IO;
+                return;
+            }
+            if (dst) dst[kZigzag[k]] = (int16_t)(int)((uint32_t)v << al);
+        } else if (r == 15) {
+            k += 15;  // ZRL
+        } else {
+            j.eobrun = (1 << r) + (r ? getbits(j, r) : 0) - 1;  // this block ends the first band of the run
+            return;
+        }
+    }
+}
+
+// one refinement bit for an already-nonzero coefficient
+inline void refine_nonzero(Jpeg &j, int16_t *cf, int p1) {
+    if (getbits(j, 1) && (*cf & p1) == 0) *cf = (int16_t)(*cf >= 0 ? *cf + p1 : *cf - p1);
+}
+
+void prog_ac_refine(Jpeg &j, const Comp &c, int16_t *dst, int ss, int se, int al) {
+    const int p1 = 1 << al;
+    int16_t scratch[64] = {0};  // a component whose coefficients are not kept: zero history
+    int16_t *b = dst ? dst : scratch;
+    int k = ss;
+    if (j.eobrun == 0) {
+        for (; k <= se; ++k) {
+            const int rs = decode_huff(j, j.ac[c.ta]);
+            int r = rs >> 4;
+            const int sz = rs & 15;
+            int v = 0;
+            if (sz) {
+                if (sz != 1) {  // a newly nonzero coefficient is +-1 at this bit position
+                    j.err = ACMMP_ERR_IO;
+                    return;
+                }
+                v = getbits(j, 1) ? p1 : -p1;
+            } else if (r != 15) {
+                j.eobrun = (1 << r) + (r ? getbits(j, r) : 0);
+                break;  // the rest of this band: EOB run logic below
+            }
+            // skip r zero-history coefficients (refining the nonzero ones passed)
+            for (; k <= se; ++k) {
+                int16_t *cf = &b[kZigzag[k]];
+                if (*cf != 0) {
+                    refine_nonzero(j, cf, p1);
+                } else if (--r < 0) {
+                    break;
+                }
+            }
+            if (v) {
+                if (k > 63) {
+                    j.err = ACMMP_ERR_IO;
+                    return;
+                }
+                b[kZigzag[k]] = (int16_t)v;
+            }
+        }
+    }
+    if (j.eobrun > 0) {  // inside an EOB run: only the refinement bits of nonzero coefficients
+        for (; k <= se; ++k) {
+            int16_t *cf = &b[kZigzag[k]];
+            if (*cf != 0) refine_nonzero(j, cf, p1);
+        }
+        --j.eobrun;
+    }
+}
+
+bool decode_scan_progressive(Jpeg &j, const int *sc, int ns, int ss, int se, int ah, int al) {
+    // T.81 G.1.1.1: DC scans cover [0, 0] (may interleave), AC scans one
+    // component and a band inside [1, 63]; refinement lowers al by one
+    if (ss > se || se > 63 || al > 13 || ah > 13 || (ah && ah != al + 1)) return false;
+    if (ss == 0 && se != 0) return false;
+    if (ss > 0 && ns != 1) return false;
+    for (int i = 0; i < ns; ++i) j.comp[sc[i]].pred = 0;  // every scan starts its DC predictions at 0
+    if (ns == 1 && j.comp[sc[0]].coef.empty()) {  // a component not kept: skip its entropy-coded data
+        while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] != 0x00 && !(j.p[1] >= 0xD0 && j.p[1] <= 0xD7))) ++j.p;
+        return true;
+    }
+    for (int i = 0; i < ns; ++i) {
+        const Comp &c = j.comp[sc[i]];
+        if (ss == 0 && ah == 0 && !j.dc[c.td].present) return false;
+        if (ss > 0 && !j.ac[c.ta].present) return false;
+    }
+    j.bitbuf = 0;
+    j.bitcnt = 0;
+    j.hit_marker = false;
+    j.eobrun = 0;
+    int mcus_x, mcus_y;
+    if (ns == 1) {  // non-interleaved: one block per MCU over the component's own extent
+        const Comp &c = j.comp[sc[0]];
+        mcus_x = (int)((j.W * (long)c.h + 8L * j.hmax - 1) / (8L * j.hmax));
+        mcus_y = (int)((j.H * (long)c.v + 8L * j.vmax - 1) / (8L * j.vmax));
+    } else {
+        mcus_x = (j.W + 8 * j.hmax - 1) / (8 * j.hmax);
+        mcus_y = (j.H + 8 * j.vmax - 1) / (8 * j.vmax);
+    }
+    int todo = j.restart;
+    for (int my = 0; my < mcus_y; ++my) {
+        for (int mx = 0; mx < mcus_x; ++mx) {
+            if (j.restart && todo == 0) {
+                handle_restart(j);
+                todo = j.restart;
+            }
+            for (int i = 0; i < ns; ++i) {
+                Comp &c = j.comp[sc[i]];
+                const int bx_n = ns == 1 ? 1 : c.h, by_n = ns == 1 ? 1 : c.v;
+                for (int by = 0; by < by_n; ++by)
+                    for (int bx = 0; bx < bx_n; ++bx) {
+                        const int gx = ns == 1 ? mx : mx * c.h + bx;
+                        const int gy = ns == 1 ? my : my * c.v + by;
+                        int16_t *dst = nullptr;
+                        if (!c.coef.empty() && gx < c.bw && gy < c.bh) dst = &c.coef[((size_t)gy * c.bw + gx) * 64];
+                        if (ss == 0) {
+                            if (ah == 0) prog_dc_first(j, c, dst, al);
+                            else prog_dc_refine(j, dst, al);
+                        } else if (ah == 0) {
+                            prog_ac_first(j, c, dst, ss, se, al);
+                        } else {
+                            prog_ac_refine(j, c, dst, ss, se, al);
+                        }
+                        if (j.err) return false;
+                    }
+            }
+            if (j.restart) --todo;
+        }
+    }
     while (j.p + 1 < j.end && !(j.p[0] == 0xFF && j.p[1] != 0x00 && !(j.p[1] >= 0xD0 && j.p[1] <= 0xD7))) ++j.p;
     return true;
 }
@@ -495,7 +665,8 @@ int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H,
         if (len < 2 || j.p + len > j.end) return ACMMP_ERR_IO;
         j.p += len;
         const int n = len - 2;
-        if (m == 0xC0 || m == 0xC1) {  // baseline / extended sequential Huffman
+        if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // baseline / extended sequential / progressive Huffman
+            j.progressive = m == 0xC2;
             if (n < 6 || seg[0] != 8) return ACMMP_ERR_UNSUPPORTED;
             j.H = u16(seg + 1);
             j.W = u16(seg + 3);
@@ -539,7 +710,7 @@ int jpeg_decode(const std::vector<uint8_t> &buf, bool size_only, int &W, int &H,
                 }
             }
         } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-            return ACMMP_ERR_UNSUPPORTED;  // progressive, lossless, arithmetic
+            return ACMMP_ERR_UNSUPPORTED;  // lossless, differential, arithmetic
         } else if (m == 0xDB) {  // DQT
             int o = 0;
             while (o < n) {

@@ -61,6 +61,9 @@ def fixtures(tmp_path_factory):
     # 16-bit quantisation tables (DQT Pq = 1, SOF1): coefficients x 2000 reach
     # the IDCT's pass-2 sums, the case its 64-bit widening is for
     Image.fromarray(g, "L").save(d / "g_q16.jpg", qtables=[[min(2000, 1 + 40 * i) for i in range(64)]])
+    # progressive (SOF2): band scans, EOB runs, refinement bits
+    Image.fromarray(g, "L").save(d / "g_prog.jpg", quality=90, progressive=True)
+    Image.fromarray(c, "RGB").save(d / "c_prog.jpg", quality=85, progressive=True, restart_marker_blocks=2)
     Image.fromarray(g, "L").save(d / "g.png")
     Image.fromarray(c, "RGB").save(d / "c.png")
     Image.fromarray(np.dstack([c, c[..., :1]]), "RGBA").save(d / "c4.png")
@@ -73,7 +76,7 @@ def fixtures(tmp_path_factory):
     return d
 
 
-IMAGES = ["g.jpg", "g_rst.jpg", "g_q16.jpg", "c420.jpg", "c444.jpg", "c422.jpg", "g.png", "c.png", "c4.png", "g16.png", "g.pgm"]
+IMAGES = ["g.jpg", "g_rst.jpg", "g_q16.jpg", "g_prog.jpg", "c_prog.jpg", "c420.jpg", "c444.jpg", "c422.jpg", "g.png", "c.png", "c4.png", "g16.png", "g.pgm"]
 
 
 @pytest.mark.parametrize("name", IMAGES)

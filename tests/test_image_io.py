@@ -56,11 +56,46 @@ def test_jpeg_grayscale_matches_libjpeg(tmp_path, w, h, q):
     np.testing.assert_array_equal(io.read_image_gray(path), _pil_gray(path))
 
 
-def test_jpeg_progressive_is_rejected(tmp_path):
+@pytest.mark.parametrize("w,h,mode,kw", [
+    (64, 48, "L", {}),                                      # gray, DC + AC band scans
+    (40, 33, "L", dict(quality=30)),                        # partial blocks, low quality
+    (123, 77, "RGB", dict(subsampling=2)),                  # 4:2:0, interleaved DC scans
+    (200, 150, "RGB", dict(subsampling=1, quality=90)),     # 4:2:2
+    (97, 131, "RGB", dict(subsampling=0, quality=100)),     # 4:4:4, many refinement bits
+    (97, 131, "RGB", dict(subsampling=2, restart_marker_blocks=3)),  # restarts reset the EOB runs
+    (301, 211, "RGB", dict(quality=75, optimize=True)),     # long EOB runs
+])
+def test_jpeg_progressive_matches_libjpeg(tmp_path, w, h, mode, kw):
+    """Progressive JPEG (SOF2): the spectral-selection and successive-
+    approximation scans of libjpeg's simple progression script — DC first,
+    AC first bands, DC and AC refinement — pixel-exact against libjpeg's
+    grayscale output and, for colour files, its RGB output (cv::imread of a
+    camera JPEG the converter copied verbatim, colmap2mvsnet_acm.py:453-454)."""
+    g = _texture(w, h, w * h + 7)
+    img = PIL.fromarray(g, "L") if mode == "L" else PIL.fromarray(np.stack([g, np.roll(g, 5, 0), 255 - g], -1), "RGB")
     path = str(tmp_path / "p.jpg")
-    PIL.fromarray(_texture(32, 32, 1), "L").save(path, "JPEG", progressive=True)
-    with pytest.raises(IOError):
-        io.read_image_gray(path)
+    img.save(path, "JPEG", progressive=True, **kw)
+    assert PIL.open(path).info.get("progressive") or PIL.open(path).info.get("progression")
+    np.testing.assert_array_equal(io.read_image_gray(path), _pil_gray(path))
+    assert io.image_size(path) == (w, h)
+    if mode == "RGB":
+        ref = np.asarray(PIL.open(path).convert("RGB"))
+        np.testing.assert_array_equal(io.read_image_bgr(path), ref[..., ::-1])
+
+
+def test_jpeg_arithmetic_and_lossless_are_rejected(tmp_path):
+    """SOF9..SOF11 (arithmetic) and SOF3 (lossless) stay unsupported: a
+    baseline file with its SOF marker rewritten must be refused, not misread."""
+    path = str(tmp_path / "b.jpg")
+    PIL.fromarray(_texture(32, 32, 1), "L").save(path, "JPEG")
+    data = bytearray(open(path, "rb").read())
+    i = data.find(b"\xff\xc0")
+    for marker in (0xC3, 0xC9, 0xCA):
+        data[i + 1] = marker
+        bad = str(tmp_path / ("m%x.jpg" % marker))
+        open(bad, "wb").write(bytes(data))
+        with pytest.raises(IOError):
+            io.read_image_gray(bad)
 
 
 def test_pgm_and_pfm(tmp_path):
