@@ -264,7 +264,9 @@ def load_library(path: str | None = None) -> C.CDLL:
         pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older A/B build without this entry point: calling it raises AttributeError
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

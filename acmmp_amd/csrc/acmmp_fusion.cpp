@@ -20,12 +20,19 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -92,6 +99,83 @@ float get_angle(const float *a, const float *b) {  // GetAngle
     if (angle != angle) return 0.0f;
     return angle;
 }
+
+// A persistent pool of acmmp_host_threads() - 1 workers: `submit` hands out
+// indices 0..n-1 of a job to whichever worker is free (dynamic rows), `wait`
+// blocks until a job is done. The caller's thread stays free for the
+// sequential approval walk, which overlaps the next view's candidate phase.
+class Pool {
+  public:
+    struct Job {
+        std::function<void(int)> fn;
+        int n = 0;
+        std::atomic<int> next{0}, done{0};
+    };
+    Pool() {
+        const int nw = std::max(1, acmmp_host_threads() - 1);
+        for (int t = 0; t < nw; ++t) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+    std::shared_ptr<Job> submit(int n, std::function<void(int)> fn) {
+        auto j = std::make_shared<Job>();
+        j->fn = std::move(fn);
+        j->n = n;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.push_back(j);
+        }
+        cv_.notify_all();
+        return j;
+    }
+    void wait(const std::shared_ptr<Job> &j) {
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return j->done.load() == j->n; });
+    }
+
+  private:
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || !jobs_.empty(); });
+                if (stop_ && jobs_.empty()) return;
+                j = jobs_.front();
+            }
+            int i;
+            bool any = false;
+            while ((i = j->next.fetch_add(1)) < j->n) {
+                j->fn(i);
+                any = true;
+                if (j->done.fetch_add(1) + 1 == j->n) {
+                    std::lock_guard<std::mutex> g(mu_);
+                    done_cv_.notify_all();
+                }
+            }
+            if (!any) {  // exhausted: retire it from the queue
+                std::lock_guard<std::mutex> g(mu_);
+                if (!jobs_.empty() && jobs_.front() == j) jobs_.pop_front();
+            }
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::deque<std::shared_ptr<Job>> jobs_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    bool stop_ = false;
+};
+
+// masks are written by the approval walk while the next view's candidate
+// phase reads them (any value read is exact, see RunFusion): relaxed atomics
+inline uint8_t mask_at(const std::vector<uint8_t> &m, size_t k) { return __atomic_load_n(&m[k], __ATOMIC_RELAXED); }
+inline void mask_set(std::vector<uint8_t> &m, size_t k) { __atomic_store_n(&m[k], (uint8_t)1, __ATOMIC_RELAXED); }
 
 // Runs fn(0..n-1) on acmmp_host_threads() threads; returns the status of the lowest
 // failing index with its message (what the sequential loop reports first).
@@ -172,6 +256,10 @@ int store_ply(const std::string &path, const std::vector<Point> &pc) {  // Store
     std::fprintf(f, "property float x\nproperty float y\nproperty float z\n");
     std::fprintf(f, "property float nx\nproperty float ny\nproperty float nz\n");
     std::fprintf(f, "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n");
+    // 27-byte records (6 floats + r, g, b) assembled in one buffer, one write
+    constexpr size_t kRec = 6 * sizeof(float) + 3;
+    std::vector<char> buf(pc.size() * kRec);
+    char *o = buf.data();
     for (const Point &p : pc) {
         F3 X = p.coord;
         const char b = (char)(int)p.color.x, g = (char)(int)p.color.y, r = (char)(int)p.color.z;
@@ -180,12 +268,14 @@ int store_ply(const std::string &path, const std::vector<Point> &pc) {  // Store
             X.x = X.y = X.z = 0.0f;
         }
         const float v[6] = {X.x, X.y, X.z, p.normal.x, p.normal.y, p.normal.z};
-        std::fwrite(v, sizeof(float), 6, f);
-        std::fwrite(&r, 1, 1, f);
-        std::fwrite(&g, 1, 1, f);
-        std::fwrite(&b, 1, 1, f);
+        std::memcpy(o, v, sizeof(v));
+        o[24] = r;
+        o[25] = g;
+        o[26] = b;
+        o += kRec;
     }
-    std::fclose(f);
+    const bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    if (std::fclose(f) != 0 || !ok) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
     return ACMMP_OK;
 }
 
@@ -214,7 +304,8 @@ CMetric metric_of(const FusionInputs &in, size_t i, int r, int c, float ref_dept
         const F3 tmp_X = world_point(src_c, src_r, src_depth, in.cameras[src]);
         float tx, ty, proj_depth;
         project(tmp_X, in.cameras[i], tx, ty, proj_depth);
-        m.reproj_err = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
+        const double dx = (double)(c - tx), dy = (double)(r - ty);  // std::pow(v, 2), exact as v * v
+        m.reproj_err = (float)std::sqrt(dx * dx + dy * dy);
         m.relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
         m.angle = get_angle(ref_normal, src_normal);
     }
@@ -291,6 +382,14 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     std::vector<int> rows(n), cols(n);
     std::map<int, int> image_id_2_index;
     for (size_t i = 0; i < n; ++i) image_id_2_index[problems[i].ref_image_id] = (int)i;
+    Pool pool;
+    const bool timing = std::getenv("ACMMP_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double>(b - a).count();
+    };
+    const auto t_start = now();
+    double t_wait = 0, t_walk = 0;
     // views load independently (JPEG decode, two .dmb reads, optional mask)
     int load_rc = parallel_for((int)n, [&](int vi) -> int {
         const size_t i = (size_t)vi;
@@ -348,129 +447,155 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     });
     if (load_rc) return load_rc;
 
-    std::vector<Point> cloud;
-    for (size_t i = 0; i < n; ++i) {
-        const int W = cols[i], H = rows[i];
-        const int num_ngb = problems[i].num_src_images;
-        const float depth_max = cameras[i].depth_max;
-        std::vector<int> used_x(num_ngb, -1), used_y(num_ngb, -1);
-        std::vector<uint8_t> approved((size_t)W * H, 0);
-        std::vector<int> src_index(num_ngb);
-        for (int j = 0; j < num_ngb; ++j) {
+    std::vector<std::vector<int>> src_index(n);
+    for (size_t i = 0; i < n; ++i)
+        for (int j = 0; j < problems[i].num_src_images; ++j) {
             auto it = image_id_2_index.find(problems[i].src_image_ids[j]);
             if (it == image_id_2_index.end())
                 return ffail(ACMMP_ERR_ARG, "source %d of view %d is not a problem", problems[i].src_image_ids[j],
                              problems[i].ref_image_id);
-            src_index[j] = it->second;
+            src_index[i].push_back(it->second);
         }
-        // Two phases per band of rows, exact to the sequential loop: (1) on
-        // host threads, every pixel's per-source projections and consistency
-        // tests against the masks as they stand (masks only ever go 0 -> 1,
-        // so a source masked now stays masked); (2) in the reference's pixel
-        // order, the sources that passed are re-checked against the current
-        // masks and accumulated in ascending j (same exp values, same sum
-        // order), then points are emitted and masks / used_list updated.
-        struct Hit {
-            int j;
-            uint32_t sp;
-            float ex;
-        };
-        const int band = 32;
-        const int ngb = std::max(num_ngb, 1);
-        std::vector<uint8_t> live((size_t)band * W);
-        std::vector<uint8_t> nhit((size_t)band * W);
-        std::vector<Hit> hits((size_t)band * W * ngb);
-        for (int r0 = 0; r0 < H; r0 += band) {
-            const int r1 = std::min(H, r0 + band);
-            parallel_for(r1 - r0, [&](int rr) -> int {
-                const int r = r0 + rr;
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c, q = (size_t)rr * W + c;
-                    live[q] = 0;
-                    nhit[q] = 0;
-                    if (masks[i][pc] == 1) continue;
+    // Two phases per view, exact to the sequential loop: (1) on the pool,
+    // every pixel's per-source projections and consistency tests against
+    // the masks as they stand (masks only ever go 0 -> 1, so a source or
+    // pixel masked when read stays masked); (2) on this thread, in the
+    // reference's pixel order, the sources that passed are re-checked
+    // against the current masks and accumulated in ascending j (same exp
+    // values, same sum order), then points are emitted and masks / used_list
+    // updated. View i + 1's phase 1 runs while view i is walked.
+    struct Hit {
+        int j;
+        uint32_t sp;
+        float ex;
+    };
+    struct ViewHits {
+        std::vector<std::vector<Hit>> row;         // hits of row r, pixel order
+        std::vector<std::vector<uint16_t>> nhit;   // hits per pixel; 0xffff = not live
+    };
+    auto phase1 = [&](size_t i, ViewHits &vh, int r) {
+        const int W = cols[i];
+        const int num_ngb = problems[i].num_src_images;
+        const float depth_max = cameras[i].depth_max;
+        std::vector<Hit> &h = vh.row[(size_t)r];
+        std::vector<uint16_t> &nh = vh.nhit[(size_t)r];
+        h.clear();
+        nh.assign((size_t)W, 0xffff);
+        for (int c = 0; c < W; ++c) {
+            const size_t pc = (size_t)r * W + c;
+            if (mask_at(masks[i], pc) == 1) continue;
+            const float ref_depth = depths[i][pc];
+            const float *ref_normal = &normals[i][pc * 3];
+            if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
+            const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
+            const size_t k0 = h.size();
+            for (int j = 0; j < num_ngb; ++j) {
+                const int s = src_index[i][j];
+                const int src_cols = cols[s], src_rows = rows[s];
+                float ptx, pty, proj_depth;
+                project(PointX, cameras[s], ptx, pty, proj_depth);
+                const int src_r = int(pty + 0.5f);
+                const int src_c = int(ptx + 0.5f);
+                if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
+                    const size_t sp = (size_t)src_r * src_cols + src_c;
+                    if (mask_at(masks[s], sp) == 1) continue;
+                    const float src_depth = depths[s][sp];
+                    const float *src_normal = &normals[s][sp * 3];
+                    if (src_depth <= 0.0) continue;
+                    const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
+                    float tx, ty;
+                    project(tmp_X, cameras[i], tx, ty, proj_depth);
+                    // std::pow(v, 2) of a float v is exact in double: v * v
+                    const double dx = (double)(c - tx), dy = (double)(r - ty);
+                    const float reproj_error = (float)std::sqrt(dx * dx + dy * dy);
+                    const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
+                    const float angle = get_angle(ref_normal, src_normal);
+                    if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
+                        const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
+                        h.push_back(Hit{j, (uint32_t)sp, std::exp(-tmp_index)});
+                    }
+                }
+            }
+            nh[(size_t)c] = (uint16_t)(h.size() - k0);
+        }
+    };
+    std::vector<ViewHits> vhits(2);
+    auto start_phase1 = [&](size_t i) {
+        ViewHits &vh = vhits[i & 1];
+        vh.row.resize((size_t)rows[i]);
+        vh.nhit.resize((size_t)rows[i]);
+        return pool.submit(rows[i], [&, i](int r) { phase1(i, vhits[i & 1], r); });
+    };
+    std::vector<Point> cloud;
+    const auto t_loaded = now();
+    auto job = start_phase1(0);
+    for (size_t i = 0; i < n; ++i) {
+        const int W = cols[i], H = rows[i];
+        const int num_ngb = problems[i].num_src_images;
+        std::vector<int> used_x(num_ngb, -1), used_y(num_ngb, -1);
+        std::vector<uint8_t> approved((size_t)W * H, 0);
+        const auto t0 = now();
+        pool.wait(job);
+        const auto t1 = now();
+        t_wait += secs(t0, t1);
+        if (i + 1 < n) job = start_phase1(i + 1);
+        const ViewHits &vh = vhits[i & 1];
+        for (int r = 0; r < H; ++r) {
+            const Hit *h = vh.row[(size_t)r].data();
+            for (int c = 0; c < W; ++c) {
+                const size_t pc = (size_t)r * W + c;
+                const int nh = vh.nhit[(size_t)r][(size_t)c];
+                if (nh == 0xffff) continue;
+                const Hit *hp = h;
+                h += nh;
+                // masks[i] changes during view i only if i is its own source
+                if (mask_at(masks[i], pc) == 1) continue;
+                int num_consistent = 0;
+                float dynamic_consistency = 0;
+                for (int k = 0; k < nh; ++k) {
+                    const int s = src_index[i][hp[k].j];
+                    if (mask_at(masks[s], hp[k].sp) == 1) continue;
+                    used_x[hp[k].j] = (int)(hp[k].sp % (uint32_t)cols[s]);
+                    used_y[hp[k].j] = (int)(hp[k].sp / (uint32_t)cols[s]);
+                    dynamic_consistency += hp[k].ex;
+                    num_consistent++;
+                }
+                if (num_consistent >= con_num_thresh && (dynamic_consistency > consistency_scalar * num_consistent)) {
                     const float ref_depth = depths[i][pc];
                     const float *ref_normal = &normals[i][pc * 3];
-                    if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
-                    live[q] = 1;
-                    const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
-                    Hit *h = &hits[q * ngb];
-                    int k = 0;
+                    const uint8_t *bgr = &images[i][pc * 3];
+                    Point p;
+                    p.coord = world_point(c, r, ref_depth, cameras[i]);
+                    p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
+                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
+                    cloud.push_back(p);
+                    // used_list is not reset per pixel in the reference: stale entries apply too
                     for (int j = 0; j < num_ngb; ++j) {
-                        const int s = src_index[j];
-                        const int src_cols = cols[s], src_rows = rows[s];
-                        float ptx, pty, proj_depth;
-                        project(PointX, cameras[s], ptx, pty, proj_depth);
-                        const int src_r = int(pty + 0.5f);
-                        const int src_c = int(ptx + 0.5f);
-                        if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
-                            const size_t sp = (size_t)src_r * src_cols + src_c;
-                            if (masks[s][sp] == 1) continue;
-                            const float src_depth = depths[s][sp];
-                            const float *src_normal = &normals[s][sp * 3];
-                            if (src_depth <= 0.0) continue;
-                            const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
-                            float tx, ty;
-                            project(tmp_X, cameras[i], tx, ty, proj_depth);
-                            const float reproj_error = (float)std::sqrt(std::pow(c - tx, 2) + std::pow(r - ty, 2));
-                            const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
-                            const float angle = get_angle(ref_normal, src_normal);
-                            if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
-                                const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                                h[k++] = Hit{j, (uint32_t)sp, std::exp(-tmp_index)};
-                            }
-                        }
-                    }
-                    nhit[q] = (uint8_t)k;
-                }
-                return (int)ACMMP_OK;
-            });
-            for (int r = r0; r < r1; ++r) {
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c, q = (size_t)(r - r0) * W + c;
-                    // masks[i] changes during view i only if i is its own source
-                    if (!live[q] || masks[i][pc] == 1) continue;
-                    int num_consistent = 0;
-                    float dynamic_consistency = 0;
-                    const Hit *h = &hits[q * ngb];
-                    for (int k = 0; k < nhit[q]; ++k) {
-                        const int s = src_index[h[k].j];
-                        if (masks[s][h[k].sp] == 1) continue;
-                        used_x[h[k].j] = (int)(h[k].sp % (uint32_t)cols[s]);
-                        used_y[h[k].j] = (int)(h[k].sp / (uint32_t)cols[s]);
-                        dynamic_consistency += h[k].ex;
-                        num_consistent++;
-                    }
-                    if (num_consistent >= con_num_thresh &&
-                        (dynamic_consistency > consistency_scalar * num_consistent)) {
-                        const float ref_depth = depths[i][pc];
-                        const float *ref_normal = &normals[i][pc * 3];
-                        const uint8_t *bgr = &images[i][pc * 3];
-                        Point p;
-                        p.coord = world_point(c, r, ref_depth, cameras[i]);
-                        p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
-                        p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
-                        cloud.push_back(p);
-                        // used_list is not reset per pixel in the reference: stale entries apply too
-                        for (int j = 0; j < num_ngb; ++j) {
-                            if (used_x[j] == -1) continue;
-                            const int s = src_index[j];
-                            masks[s][(size_t)used_y[j] * cols[s] + used_x[j]] = 1;
-                            // `approved` is this view's W x H image indexed by source coordinates (:1030)
-                            if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
-                        }
+                        if (used_x[j] == -1) continue;
+                        const int s = src_index[i][j];
+                        mask_set(masks[s], (size_t)used_y[j] * cols[s] + used_x[j]);
+                        // `approved` is this view's W x H image indexed by source coordinates (:1030)
+                        if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
                     }
                 }
             }
         }
+        t_walk += secs(t1, now());
         if (write_debug_images) {
             const std::string dbg = dense + "/approved_pixels_cam_" + std::to_string(i) + ".png";
-            if (acmmp_internal_write_png(dbg.c_str(), W, H, 1, approved.data()))
+            if (acmmp_internal_write_png(dbg.c_str(), W, H, 1, approved.data())) {
+                if (i + 1 < n) pool.wait(job);
                 return ffail(ACMMP_ERR_IO, "cannot write %s", dbg.c_str());
+            }
         }
     }
     if (num_points) *num_points = (int)cloud.size();
-    return store_ply(out + "/ACMMP_model.ply", cloud);
+    const auto t_walked = now();
+    const int rc = store_ply(out + "/ACMMP_model.ply", cloud);
+    if (timing)
+        std::fprintf(stderr, "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d\n",
+                     secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), acmmp_host_threads());
+    return rc;
 }
 
 int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_folder, const char *fusion_folder,
@@ -536,6 +661,7 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         masks[i].assign((size_t)w * h, 0);
     }
     std::vector<Point> cloud;
+    Pool pool;
     // Same two-phase scheme as RunFusion: candidates (projection + metrics of
     // both maps) per band of rows on host threads against the current masks,
     // then the reference's pixel order with every approval re-checked
@@ -560,7 +686,7 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         std::vector<Ok> oks((size_t)band * W * 2 * ns);
         for (int r0 = 0; r0 < H; r0 += band) {
             const int r1 = std::min(H, r0 + band);
-            parallel_for(r1 - r0, [&](int rr) -> int {
+            pool.wait(pool.submit(r1 - r0, [&](int rr) {
                 const int r = r0 + rr;
                 std::vector<CInfo> cand;
                 for (int c = 0; c < W; ++c) {
@@ -585,8 +711,7 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
                     }
                     state[q] = st;
                 }
-                return (int)ACMMP_OK;
-            });
+            }));
             for (int r = r0; r < r1; ++r) {
                 for (int c = 0; c < W; ++c) {
                     const size_t pc = (size_t)r * W + c, q = (size_t)(r - r0) * W + c;

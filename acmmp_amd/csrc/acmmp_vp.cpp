@@ -283,7 +283,7 @@ std::string result_folder(const std::string &out, int ref_id) {
 struct ViewState {
     DevBuf planes, costs;  // (H, W, 4) world normal + depth, (H, W)
     int W = 0, H = 0;
-    std::vector<float> jbu;  // upsampled depth of the hierarchy pass (host)
+    DevBuf jbu;  // upsampled depth of the hierarchy pass (device, the next scale's W x H)
 };
 
 // --------------------------------------------------------------- driver
@@ -348,8 +348,8 @@ class Driver {
                 }
             {
                 Clock c(this, "load");
-                load_views();
                 shapes();
+                load_views();
             }
             if (first) {
                 first = false;
@@ -419,12 +419,16 @@ class Driver {
             });
     }
 
+    // Images of this scale, decoded once per node: every rank decodes the
+    // reference images of ITS views (acmmp_load_view: JPEG decode + rescale,
+    // InputInitialization src/ACMMP.cpp:536-598) and the images travel in
+    // ONE padded all-gather, like the depth maps (RCCL over xGMI); cameras
+    // come from the headers and cam files of every image a view needs.
     void load_views() {
         for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
         textures_.clear();
         images_.clear();
         cams_.clear();
-        host_images_.clear();
         std::vector<int> need;
         for (int v : mine_) {
             const acmmp_problem &p = problems_[(size_t)v];
@@ -433,49 +437,70 @@ class Driver {
         }
         std::sort(need.begin(), need.end());
         need.erase(std::unique(need.begin(), need.end()), need.end());
-        std::vector<std::vector<float>> host(need.size());
+        for (int id : need)
+            if (!index_of_.count(id)) fail("source id " + std::to_string(id) + " is not a problem index");
+        // work items: the cameras of every needed image, the pixels of my refs
         std::vector<acmmp_camera> cams(need.size());
-        std::vector<std::string> errs(need.size());
+        std::vector<std::vector<float>> host(mine_.size());
+        std::vector<acmmp_camera> own_cams(mine_.size());
+        const size_t nwork = need.size() + mine_.size();
+        std::vector<std::string> errs(nwork);
         std::atomic<size_t> next{0};
         auto worker = [&]() {
-            for (size_t k; (k = next++) < need.size();) {
-                const int id = need[k];
-                auto it = index_of_.find(id);
-                if (it == index_of_.end()) {
-                    errs[k] = "source id " + std::to_string(id) + " is not a problem index";
-                    continue;
-                }
-                const int size = problems_[(size_t)it->second].cur_image_size;
-                int rc = acmmp_load_view(o_.dense.c_str(), id, size, nullptr, 0, &cams[k]);
+            for (size_t k; (k = next++) < nwork;) {
+                const bool pixels = k >= need.size();
+                const int v = pixels ? mine_[k - need.size()] : -1;
+                const int id = pixels ? problems_[(size_t)v].ref_image_id : need[k];
+                acmmp_camera &cam = pixels ? own_cams[k - need.size()] : cams[k];
+                const int size = problems_[(size_t)index_of_.at(id)].cur_image_size;
+                int rc = acmmp_load_view(o_.dense.c_str(), id, size, nullptr, 0, &cam);
                 if (rc != ACMMP_OK && rc != ACMMP_ERR_ARG) {
                     errs[k] = std::string("acmmp_load_view: ") + acmmp_pipeline_last_error();
                     continue;
                 }
-                host[k].resize((size_t)cams[k].width * cams[k].height);
-                rc = acmmp_load_view(o_.dense.c_str(), id, size, host[k].data(), host[k].size(), &cams[k]);
+                if (!pixels) continue;
+                std::vector<float> &h = host[k - need.size()];
+                h.resize((size_t)cam.width * cam.height);
+                rc = acmmp_load_view(o_.dense.c_str(), id, size, h.data(), h.size(), &cam);
                 if (rc != ACMMP_OK) errs[k] = std::string("acmmp_load_view: ") + acmmp_pipeline_last_error();
             }
         };
         std::vector<std::thread> pool;
-        const int nt = (int)std::min<size_t>((size_t)acmmp_host_threads(), need.size());
+        const int nt = (int)std::min<size_t>((size_t)acmmp_host_threads(), nwork);
         for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
         for (auto &t : pool) t.join();
-        for (size_t k = 0; k < need.size(); ++k)
-            if (!errs[k].empty()) fail("view " + std::to_string(need[k]) + ": " + errs[k]);
-        for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
-        textures_.clear();
-        for (size_t k = 0; k < need.size(); ++k) {
+        for (size_t k = 0; k < nwork; ++k)
+            if (!errs[k].empty())
+                fail("view " + std::to_string(k < need.size() ? need[k] : problems_[(size_t)mine_[k - need.size()]].ref_image_id) +
+                     ": " + errs[k]);
+        // my refs: kept contiguous for JBU, and padded into my all-gather slots
+        DevBuf send((size_t)slots_ * hmax_ * wmax_);
+        hip_check(hipMemset(send.p, 0, send.n * sizeof(float)), "hipMemset");
+        for (size_t k = 0; k < mine_.size(); ++k) {
+            const acmmp_camera &c = own_cams[k];
+            const int v = mine_[k];
+            if (c.height != shape_[(size_t)v].first || c.width != shape_[(size_t)v].second)
+                fail("view " + std::to_string(problems_[(size_t)v].ref_image_id) + ": image size disagrees with its header");
             DevBuf d(host[k].size());
-            hip_check(hipMemcpy(d.p, host[k].data(), host[k].size() * sizeof(float), hipMemcpyHostToDevice),
-                      "hipMemcpy");
-            // the padded footprint records, built once per image and scale
+            hip_check(hipMemcpy(d.p, host[k].data(), host[k].size() * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
+            hip_check(hipMemcpy2D(send.p + k * (size_t)hmax_ * wmax_, (size_t)wmax_ * sizeof(float), d.p,
+                                  (size_t)c.width * sizeof(float), (size_t)c.width * sizeof(float), (size_t)c.height,
+                                  hipMemcpyDeviceToDevice),
+                      "hipMemcpy2D");
+            images_.emplace(problems_[(size_t)v].ref_image_id, std::move(d));
+        }
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        recv_img_ = DevBuf(send.n * (size_t)g_.world);
+        ex_.allgather(send.p, recv_img_.p, send.n);
+        // the padded footprint records, built once per image and scale from
+        // the gathered image (row pitch Wmax)
+        for (size_t k = 0; k < need.size(); ++k) {
+            const acmmp_camera &c = cams[k];
+            const float *img = gathered_in(recv_img_, index_of_.at(need[k]));
             acmmp_texture *t = nullptr;
-            acmmp_check(acmmp_texture_create(o_.device, d.p, cams[k].width, cams[k].width, cams[k].height, &t),
-                        "acmmp_texture_create");
+            acmmp_check(acmmp_texture_create(o_.device, img, wmax_, c.width, c.height, &t), "acmmp_texture_create");
             textures_[need[k]] = t;
-            images_.emplace(need[k], std::move(d));
-            cams_[need[k]] = cams[k];
-            host_images_[need[k]] = std::move(host[k]);
+            cams_[need[k]] = c;
         }
     }
 
@@ -523,15 +548,17 @@ class Driver {
         return p;
     }
 
-    // the gathered depth map of problem i (previous pass) and its pitch
-    const float *gathered(int i) const {
+    // problem i's map in a padded all-gather buffer (row pitch Wmax)
+    const float *gathered_in(const DevBuf &buf, int i) const {
         for (int r = 0; r < g_.world; ++r) {
             const auto &a = assignment_[(size_t)r];
             for (size_t k = 0; k < a.size(); ++k)
-                if (a[k] == i) return recv_.p + ((size_t)r * slots_ + k) * hmax_ * wmax_;
+                if (a[k] == i) return buf.p + ((size_t)r * slots_ + k) * hmax_ * wmax_;
         }
         fail("view not assigned");
     }
+    // the gathered depth map of problem i (previous pass)
+    const float *gathered(int i) const { return gathered_in(recv_, i); }
 
     void compute(acmmp_ctx *eng, const Task &t, ViewState &out) {
         const acmmp_problem &pr = problems_[(size_t)t.v];
@@ -561,21 +588,21 @@ class Driver {
             acmmp_check(acmmp_set_plane_hypotheses_device(eng, prev.planes.p, prev.costs.p),
                         "acmmp_set_plane_hypotheses_device", eng);
         }
+        DevBuf scaled;  // alive until the run below has been synchronised
         if (t.hier) {  // scaled planes = previous scale's normals + (costs, or the JBU depth when no upsample)
             const int sh = prev.H, sw = prev.W;
-            std::vector<float> pl((size_t)sh * sw * 4), co((size_t)sh * sw);
-            hip_check(hipMemcpy(pl.data(), prev.planes.p, pl.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
-            hip_check(hipMemcpy(co.data(), prev.costs.p, co.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+            const size_t S = (size_t)sh * sw;
             const bool upsample = sw != H || sh != W;  // src/ACMMP.cpp:766, rows/cols swap included
-            std::vector<float> scaled(pl.size());
-            for (size_t k = 0; k < (size_t)sh * sw; ++k) {
-                scaled[4 * k + 0] = pl[4 * k + 0];
-                scaled[4 * k + 1] = pl[4 * k + 1];
-                scaled[4 * k + 2] = pl[4 * k + 2];
-                scaled[4 * k + 3] = upsample ? co[k] : prev.jbu[k];
-            }
-            acmmp_check(acmmp_set_hierarchy_inputs(eng, scaled.data(), sw, sh, prev.jbu.data()),
-                        "acmmp_set_hierarchy_inputs", eng);
+            if (!upsample && prev.jbu.n < S) fail("hierarchy input: JBU depth smaller than the scaled planes");
+            scaled = DevBuf(S * 4);
+            // built on the device: the normals, then the 4th channel as a
+            // strided copy (4 of every 16 bytes), as the Python driver does
+            hip_check(hipMemcpy(scaled.p, prev.planes.p, S * 4 * sizeof(float), hipMemcpyDeviceToDevice), "hipMemcpy");
+            hip_check(hipMemcpy2D(scaled.p + 3, 4 * sizeof(float), upsample ? prev.costs.p : prev.jbu.p, sizeof(float),
+                                  sizeof(float), S, hipMemcpyDeviceToDevice),
+                      "hipMemcpy2D");
+            acmmp_check(acmmp_set_hierarchy_inputs_device(eng, scaled.p, sw, sh, prev.jbu.p),
+                        "acmmp_set_hierarchy_inputs_device", eng);
         }
         acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
         if (t.planar) {
@@ -668,22 +695,23 @@ class Driver {
     }
 
     // JointBilateralUpsampling of each owned view's previous-scale depth to
-    // this scale's image (src/ACMMP.cpp:964-1087), kept for the hierarchy pass
+    // this scale's image (src/ACMMP.cpp:964-1087) on the device, kept there
+    // for the hierarchy pass
     void jbu() {
         for (int v : mine_) {
             ViewState &s = state_[v];
             const int id = problems_[(size_t)v].ref_image_id;
             const acmmp_camera &c = cams_.at(id);
-            const std::vector<float> &img = host_images_.at(id);
             const size_t P = (size_t)s.W * s.H;
-            std::vector<float> pl(P * 4), d(P);
-            hip_check(hipMemcpy(pl.data(), s.planes.p, pl.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
-            for (size_t k = 0; k < P; ++k) d[k] = pl[4 * k + 3];
-            s.jbu.assign((size_t)c.width * c.height, 0.0f);
+            DevBuf d(P);  // the depth channel of the previous scale's planes
+            hip_check(hipMemcpy2D(d.p, sizeof(float), s.planes.p + 3, 4 * sizeof(float), sizeof(float), P,
+                                  hipMemcpyDeviceToDevice),
+                      "hipMemcpy2D");
+            s.jbu = DevBuf((size_t)c.width * c.height);
             int isc = 0;
-            acmmp_check(acmmp_joint_bilateral_upsample(o_.device, img.data(), c.width, c.height, d.data(), s.W, s.H,
-                                                       s.jbu.data(), &isc),
-                        "acmmp_joint_bilateral_upsample");
+            acmmp_check(acmmp_joint_bilateral_upsample_device(o_.device, images_.at(id).p, c.width, c.height, d.p, s.W,
+                                                              s.H, s.jbu.p, &isc),
+                        "acmmp_joint_bilateral_upsample_device");
             if (isc <= 1) fail("view " + std::to_string(id) + ": JBU image scale 1 (nothing to upsample)");
         }
     }
@@ -701,10 +729,10 @@ class Driver {
     std::map<int, DevBuf> images_;
     std::map<int, acmmp_texture *> textures_;  // ~ the reference's texture objects, per image and scale
     std::map<int, acmmp_camera> cams_;
-    std::map<int, std::vector<float>> host_images_;
     std::vector<std::pair<int, int>> shape_;
     int slots_ = 1, hmax_ = 0, wmax_ = 0;
     DevBuf send_, recv_;
+    DevBuf recv_img_;  // this scale's images of every view, gathered (textures borrow it)
     std::map<int, DevBuf> depth_tmp_;
     std::map<int, ViewState> state_;
     std::mutex mu_;

@@ -264,7 +264,10 @@ class ViewParallelPipeline:
 
     def _load_views(self):
         """Images + cameras of every image my views need, at their problem's
-        cur_image_size (InputInitialization, src/ACMMP.cpp:536-598)."""
+        cur_image_size (InputInitialization, src/ACMMP.cpp:536-598), decoded
+        once per node: each rank decodes the reference images of ITS views
+        and one padded all-gather (RCCL over xGMI, like the depth maps)
+        hands every rank all of them; the cameras come from the headers."""
         import ctypes as C
         lib = _abi.load_library()
         need = set()
@@ -272,17 +275,19 @@ class ViewParallelPipeline:
             p = self.problems[v]
             need.add(p.ref_image_id)
             need.update(p.sources)
-        self.images, self.cams = {}, {}
         for i in sorted(need):
             if i not in self.index_of:
                 raise AcmmpError(f"source id {i} is not a problem index (pair.txt ids must be 0..n-1)")
 
-        def load(i):  # on a pool thread: the library call drops the GIL; its error slot is per thread
+        def load(item):  # on a pool thread: the library call drops the GIL; its error slot is per thread
+            i, pixels = item
             size = self.problems[self.index_of[i]].cur_image_size
             cam = _abi.Camera()
             rc = lib.acmmp_load_view(self.dense.encode(), i, size, None, 0, C.byref(cam))
             if rc not in (0, _abi.ERR_ARG):
                 raise AcmmpError(f"acmmp_load_view({i}) failed: {lib.acmmp_pipeline_last_error().decode()}")
+            if not pixels:
+                return None, cam
             img = np.empty((cam.height, cam.width), dtype=np.float32)
             rc = lib.acmmp_load_view(self.dense.encode(), i, size, img.ctypes.data_as(C.POINTER(C.c_float)),
                                      img.size, C.byref(cam))
@@ -292,11 +297,20 @@ class ViewParallelPipeline:
 
         from concurrent.futures import ThreadPoolExecutor
         order = sorted(need)
-        with ThreadPoolExecutor(max_workers=max(1, min(lib.acmmp_host_threads(), len(order)))) as ex:
-            loaded = list(ex.map(load, order))  # re-raises the first failure in id order
-        for i, (img, cam) in zip(order, loaded):
-            self.images[i] = torch.from_numpy(img).to(self.tdev)
-            self.cams[i] = cam
+        own = [self.problems[v].ref_image_id for v in self.mine]
+        work = [(i, False) for i in order] + [(i, True) for i in own]
+        with ThreadPoolExecutor(max_workers=max(1, min(lib.acmmp_host_threads(), len(work)))) as ex:
+            loaded = list(ex.map(load, work))  # re-raises the first failure in id order
+        self.cams = {i: cam for i, (_, cam) in zip(order, loaded[:len(order)])}
+        mine_imgs = {v: torch.from_numpy(img) for v, (img, _) in zip(self.mine, loaded[len(order):])}
+        shapes = self._shapes()
+        for v, img in mine_imgs.items():
+            if tuple(img.shape) != shapes[v]:
+                raise AcmmpError(f"view {self.problems[v].ref_image_id}: image size disagrees with its header")
+        gathered = DepthExchange(self.assignment, shapes, self.cdev, self.group,
+                                 out_device=self.tdev).gather(self.rank, mine_imgs)
+        # pitched views into the gathered buffer (row pitch Wmax)
+        self.images = {i: gathered[self.index_of[i]] for i in order}
         self._sync()
         # one texture (padded footprint records) per image and scale, shared by
         # every view and pass of the scale (engine runs only)

@@ -16,7 +16,13 @@ Synthetic, seeded scene rendered on the GPU and written as 8-bit JPEGs (a
 COLMAP-converted dense folder); wall times include JPEG decode and .dmb I/O,
 as the reference's do. Iterations: the driver's default (the reference's).
 usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] [steps] > gpurun_out/pipeline.jsonl
-  steps: comma list of distributed,cli_vp,cli,fusion (default distributed,cli,fusion; fusion needs cli)
+  steps: comma list of distributed,cli_vp,cli,fusion,fusion_dist (default distributed,cli,fusion;
+         fusion fuses the CLI's maps, fusion_dist the distributed driver's, once per library in
+         ACMMP_FUSION_LIBS (comma list, default the product) in a subprocess each)
+
+The 49 views sit 1.8 degrees apart on the arc (86 degrees in all, like a DTU
+scan; r01/r02 used 6 degrees, which wraps 288 degrees round the object and
+leaves some views looking at the scene edge-on).
 """
 import json
 import os
@@ -34,6 +40,7 @@ import torch  # noqa: E402
 from acmmp_amd import scene  # noqa: E402
 from acmmp_amd import pipeline  # noqa: E402
 from acmmp_amd.distributed import ViewParallelPipeline  # noqa: E402
+from acmmp_amd import load_library as _lib  # noqa: E402
 
 V = int(sys.argv[1]) if len(sys.argv) > 1 else 49
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 1600
@@ -48,7 +55,7 @@ def emit(**kw):
 
 def main():
     dev = torch.device("cuda", 0)
-    setup = scene.scene_setup(num_views=V, width=W, height=H)
+    setup = scene.scene_setup(num_views=V, width=W, height=H, arc_deg=float(os.environ.get("ACMMP_ARC_DEG", "1.8")))
     views = []
     for i in range(V):
         img = scene.render_torch(setup, i, dev).cpu().numpy()
@@ -73,6 +80,18 @@ def main():
         emit(step="distributed_world1", order="jacobi", concurrent_views=2, s=round(wall, 2),
              gpu_runpatchmatch_s=round(pipe.gpu_ms / 1e3, 2),
              phases_s={k: round(v, 2) for k, v in sorted(pipe.phase_s.items())})
+        if "fusion_dist" in STEPS:
+            for lib in os.environ.get("ACMMP_FUSION_LIBS", os.path.join(ROOT, "acmmp_amd", "lib",
+                                                                         "libacmmp_amd.so")).split(","):
+                code = ("import sys, time, json; sys.path.insert(0, %r); from acmmp_amd import pipeline; "
+                        "t0 = time.perf_counter(); n = pipeline.run_fusion(%r, %r); "
+                        "print(json.dumps({'points': n, 's': round(time.perf_counter() - t0, 2)}))"
+                        % (ROOT, dense, dense + "/ACMMP_dist"))
+                r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
+                                   env=dict(os.environ, ACMMP_LIB=lib))
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+                emit(step="fusion_of_distributed_maps", lib=os.path.basename(lib), points=res["points"], s=res["s"],
+                     host_threads=int(_lib().acmmp_host_threads()))
         shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
     if "cli_vp" in STEPS:  # the C++ view-parallel driver, world 1 through RCCL
         cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
