@@ -139,6 +139,20 @@ class PassOptions(C.Structure):
 
 _FP = C.POINTER(C.c_float)
 _U32P = C.POINTER(C.c_uint32)
+class BandHalo(C.Structure):
+    """acmmp_band_halo (include/acmmp.h): the rows one half-sweep of a
+    row-band split run exchanges with the neighbouring bands."""
+    _fields_ = [("colour", C.c_int32), ("Wh", C.c_int32), ("plane", C.c_void_p), ("cost", C.c_void_p),
+                ("sv", C.c_void_p), ("stream", C.c_void_p),
+                ("send_up_lo", C.c_int32), ("send_up_hi", C.c_int32),
+                ("send_down_lo", C.c_int32), ("send_down_hi", C.c_int32),
+                ("recv_up_lo", C.c_int32), ("recv_up_hi", C.c_int32),
+                ("recv_down_lo", C.c_int32), ("recv_down_hi", C.c_int32)]
+
+
+BAND_HALO = 23  # ACMMP_BAND_HALO
+BandExchangeFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(BandHalo))
+
 _CTX = C.c_void_p
 
 # name -> (restype, argtypes)
@@ -182,6 +196,7 @@ SIGNATURES = {
     "acmmp_run_patchmatch": (C.c_int, [_CTX]),
     "acmmp_run_patchmatch_async": (C.c_int, [_CTX]),
     "acmmp_synchronize": (C.c_int, [_CTX]),
+    "acmmp_run_patchmatch_band": (C.c_int, [_CTX, C.c_int, C.c_int, BandExchangeFn, C.c_void_p]),
     "acmmp_get_plane_hypotheses": (C.c_int, [_CTX, _FP, C.c_size_t]),
     "acmmp_get_costs": (C.c_int, [_CTX, _FP, C.c_size_t]),
     "acmmp_get_selected_views": (C.c_int, [_CTX, _U32P, C.c_size_t]),

@@ -144,8 +144,11 @@ int kv_upload(acmmp_ctx *ctx) {
     return ACMMP_OK;
 }
 
-KState state_of(acmmp_ctx *ctx) {
+// y0, y1: the image rows a launch covers (all rows by default)
+KState state_of(acmmp_ctx *ctx, int y0 = 0, int y1 = -1) {
     KState st{};
+    st.y0 = y0;
+    st.y1 = y1 < 0 ? ctx->H : y1;
     for (int c = 0; c < 2; ++c) {
         st.plane[c] = ctx->d_cplane[c][ctx->cur[c]];
         st.cost[c] = ctx->d_ccost[c][ctx->cur[c]];
@@ -738,7 +741,10 @@ int acmmp_set_planar_prior(acmmp_ctx *ctx, const float *plane_params4, int num_p
     return ACMMP_OK;
 }
 
-int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
+namespace {
+// The checks and constant upload every run starts with (RunPatchMatch's
+// preconditions, src/ACMMP.cu:1378-1414).
+int prepare_run(acmmp_ctx *ctx) {
     int rc = check_ready(ctx);
     if (rc) return rc;
     const acmmp_params &p = ctx->prm;
@@ -761,6 +767,14 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
         for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
         ctx->events_made = true;
     }
+    return ACMMP_OK;
+}
+}  // namespace
+
+int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
+    int rc = prepare_run(ctx);
+    if (rc) return rc;
+    const acmmp_params &p = ctx->prm;
     hipStream_t s = ctx->stream;
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
     ctx->cur[0] = ctx->cur[1] = 0;
@@ -780,6 +794,60 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     ctx->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
     ctx->have_state = true;
     return ACMMP_OK;
+}
+
+int acmmp_run_patchmatch_band(acmmp_ctx *ctx, int row_lo, int row_hi, acmmp_band_exchange_fn exchange, void *user) {
+    int rc = prepare_run(ctx);
+    if (rc) return rc;
+    const int H = ctx->H, K = ACMMP_BAND_HALO;
+    if (!exchange || row_lo < 0 || row_hi > H || row_lo >= row_hi)
+        return set_err(ctx, ACMMP_ERR_ARG, "band rows [%d, %d) outside [0, %d) or no exchange", row_lo, row_hi, H);
+    const acmmp_params &p = ctx->prm;
+    hipStream_t s = ctx->stream;
+    const int lo_k = std::max(0, row_lo - K), hi_k = std::min(H, row_hi + K);
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
+    ctx->cur[0] = ctx->cur[1] = 0;
+    // every pixel's initial state is a function of its own inputs: computing
+    // the halo rows here too means they start out valid, with no exchange
+    HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, state_of(ctx, lo_k, hi_k), s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[1], s));
+    acmmp_band_halo halo{};
+    halo.Wh = ctx->Wh;
+    halo.stream = (void *)s;
+    halo.send_up_lo = row_lo;
+    halo.send_up_hi = row_lo > 0 ? std::min(row_hi, row_lo + K) : row_lo;
+    halo.send_down_lo = row_hi < H ? std::max(row_lo, row_hi - K) : row_hi;
+    halo.send_down_hi = row_hi;
+    halo.recv_up_lo = lo_k;
+    halo.recv_up_hi = row_lo;
+    halo.recv_down_lo = row_hi;
+    halo.recv_down_hi = hi_k;
+    for (int it = 0; it < p.max_iterations; ++it) {
+        for (int colour = 0; colour < 2; ++colour) {
+            HIP_TRY(ctx, launch_sweep(ctx->d_kv, ctx->h_kv, state_of(ctx, row_lo, row_hi), colour, it, s));
+            ctx->cur[colour] ^= 1;
+            // the colour's new current state: the neighbours' rows next to
+            // the band, as the next half-sweeps read them
+            halo.colour = colour;
+            halo.plane = ctx->d_cplane[colour][ctx->cur[colour]];
+            halo.cost = ctx->d_ccost[colour][ctx->cur[colour]];
+            halo.sv = ctx->d_csv[colour];
+            if (const int e = exchange(user, &halo))
+                return set_err(ctx, ACMMP_ERR_STATE, "band exchange failed (status %d) after iteration %d colour %d", e,
+                               it, colour);
+        }
+    }
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[2], s));
+    // CheckerboardFilter reads +-5 rows (src/ACMMP.cu:1214-1328): depth /
+    // normal conversion on the band +-10 rows (valid halos), the black filter
+    // on the band +-5 rows (what the red filter reads), the red one on the band
+    HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, state_of(ctx, std::max(0, row_lo - 10), std::min(H, row_hi + 10)), s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx, std::max(0, row_lo - 5), std::min(H, row_hi + 5)), 0, s));
+    HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx, row_lo, row_hi), 1, s));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
+    ctx->prm.rng_stream += 1u;
+    ctx->have_state = true;
+    return acmmp_synchronize(ctx);
 }
 
 int acmmp_synchronize(acmmp_ctx *ctx) {

@@ -172,10 +172,20 @@ class Pool {
     bool stop_ = false;
 };
 
-// masks are written by the approval walk while the next view's candidate
-// phase reads them (any value read is exact, see RunFusion): relaxed atomics
-inline uint8_t mask_at(const std::vector<uint8_t> &m, size_t k) { return __atomic_load_n(&m[k], __ATOMIC_RELAXED); }
-inline void mask_set(std::vector<uint8_t> &m, size_t k) { __atomic_store_n(&m[k], (uint8_t)1, __ATOMIC_RELAXED); }
+// RunFusion's per-view masks as bitsets: a view's ~20 sources' masks then
+// stay cache-resident during the approval walk (1 bit instead of 1 byte a
+// pixel). The walk is their only writer; the next view's candidate phase
+// reads them meanwhile (any value read is exact, see RunFusion): relaxed
+// atomic words.
+struct MaskBits {
+    std::vector<uint64_t> w;
+    void assign(size_t n) { w.assign((n + 63) / 64, 0ull); }
+    bool get(size_t k) const { return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull; }
+    void set(size_t k) {  // single writer
+        const uint64_t v = __atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) | (1ull << (k & 63));
+        __atomic_store_n(&w[k >> 6], v, __ATOMIC_RELAXED);
+    }
+};
 
 // Runs fn(0..n-1) on acmmp_host_threads() threads; returns the status of the lowest
 // failing index with its message (what the sequential loop reports first).
@@ -376,7 +386,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     const std::string cam_folder = dense + "/cams";
     const bool use_masks = mask_folder && std::string(mask_folder) != " " && mask_folder[0] != 0;
     const size_t n = (size_t)count;
-    std::vector<std::vector<uint8_t>> images(n), masks(n);
+    std::vector<std::vector<uint8_t>> images(n);
+    std::vector<MaskBits> masks(n);
     std::vector<acmmp_camera> cameras(n);
     std::vector<std::vector<float>> depths(n), normals(n);
     std::vector<int> rows(n), cols(n);
@@ -427,7 +438,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             cameras[i].width = w;
             cameras[i].height = h;
         }
-        masks[i].assign((size_t)w * h, 0);
+        masks[i].assign((size_t)w * h);
         if (use_masks) {  // :881-905: mask = (resize(mask) < 128) / 255
             const std::string mpath = dense + "/" + mask_folder + "/" + id8(id) + ".png";
             int mw = 0, mh = 0, mc = 0, bd = 0;
@@ -441,7 +452,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             std::vector<uint8_t> m8((size_t)mw * mh), mr;
             for (size_t k = 0; k < m8.size(); ++k) m8[k] = (uint8_t)m16[k * mc];
             resize_u8(m8, mw, mh, 1, mr, w, h);
-            for (size_t k = 0; k < mr.size(); ++k) masks[i][k] = mr[k] < 128 ? 1 : 0;
+            for (size_t k = 0; k < mr.size(); ++k)
+                if (mr[k] < 128) masks[i].set(k);
         }
         return (int)ACMMP_OK;
     });
@@ -483,7 +495,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         nh.assign((size_t)W, 0xffff);
         for (int c = 0; c < W; ++c) {
             const size_t pc = (size_t)r * W + c;
-            if (mask_at(masks[i], pc) == 1) continue;
+            if (masks[i].get(pc)) continue;
             const float ref_depth = depths[i][pc];
             const float *ref_normal = &normals[i][pc * 3];
             if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
@@ -498,7 +510,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 const int src_c = int(ptx + 0.5f);
                 if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
                     const size_t sp = (size_t)src_r * src_cols + src_c;
-                    if (mask_at(masks[s], sp) == 1) continue;
+                    if (masks[s].get(sp)) continue;
                     const float src_depth = depths[s][sp];
                     const float *src_normal = &normals[s][sp * 3];
                     if (src_depth <= 0.0) continue;
@@ -549,12 +561,12 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 const Hit *hp = h;
                 h += nh;
                 // masks[i] changes during view i only if i is its own source
-                if (mask_at(masks[i], pc) == 1) continue;
+                if (masks[i].get(pc)) continue;
                 int num_consistent = 0;
                 float dynamic_consistency = 0;
                 for (int k = 0; k < nh; ++k) {
                     const int s = src_index[i][hp[k].j];
-                    if (mask_at(masks[s], hp[k].sp) == 1) continue;
+                    if (masks[s].get(hp[k].sp)) continue;
                     used_x[hp[k].j] = (int)(hp[k].sp % (uint32_t)cols[s]);
                     used_y[hp[k].j] = (int)(hp[k].sp / (uint32_t)cols[s]);
                     dynamic_consistency += hp[k].ex;
@@ -573,7 +585,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     for (int j = 0; j < num_ngb; ++j) {
                         if (used_x[j] == -1) continue;
                         const int s = src_index[i][j];
-                        mask_set(masks[s], (size_t)used_y[j] * cols[s] + used_x[j]);
+                        masks[s].set((size_t)used_y[j] * cols[s] + used_x[j]);
                         // `approved` is this view's W x H image indexed by source coordinates (:1030)
                         if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
                     }

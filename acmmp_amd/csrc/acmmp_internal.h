@@ -78,6 +78,7 @@ struct KState {
     const uint32_t *mask;   // planar prior triangle labels
     const float4 *scaled;   // hierarchy low-res planes (scaled_rows x scaled_cols)
     const float4 *seed;     // seeded priors
+    int y0, y1;             // image rows [y0, y1) a launch covers (all rows, or a band; acmmp_run_patchmatch_band)
 };
 
 // Kernel launchers (acmmp_kernels.hip). All enqueue on `stream`.

@@ -831,7 +831,7 @@ struct BlockXY {
     int bx, by;
 };
 
-DEV BlockXY xcd_block() {
+DEV BlockXY xcd_block(int by0 = 0) {  // by0: block row of the grid's first row (row bands)
     const int gx = gridDim.x;
     const int T = gx * gridDim.y;
     const int L = blockIdx.y * gx + blockIdx.x;
@@ -841,6 +841,7 @@ DEV BlockXY xcd_block() {
     BlockXY b;
     b.by = nl / gx;
     b.bx = nl - b.by * gx;
+    b.by += by0;
     return b;
 }
 
@@ -873,12 +874,12 @@ __global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KS
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
-    const BlockXY blk = xcd_block();
+    const BlockXY blk = xcd_block(st.y0 / kBY);
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
     const int px = g.px, py = g.py;
-    if (px >= kv.W || py >= kv.H) return;
+    if (px >= kv.W || py < st.y0 || py >= st.y1) return;
     const acmmp_params &prm = kv.prm;
     const acmmp_camera &c0 = kv.cam[0];
     const int center = py * kv.W + px;
@@ -1058,13 +1059,13 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     __shared__ WSlot wlds[kSlots * kThreads];
     __shared__ float4 cand_lds[8 * kThreads];
     const KViews &kv = *kvp;
-    const BlockXY blk = xcd_block();
+    const BlockXY blk = xcd_block(st.y0 / kBY);
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
     const int px = g.px, py = g.py;
     const int width = kv.W, height = kv.H;
-    if (py >= height || px >= width) return;
+    if (py < st.y0 || py >= st.y1 || px >= width) return;  // rows [y0, y1) of the image (a band or all)
     const int oc = colour ^ 1;
     const int Wh = kv.Wh;
     const int my = py * Wh + g.k;
@@ -1549,8 +1550,8 @@ __global__ __launch_bounds__(256, kSweepWaves) void k_sweep_f(const KViews *__re
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
     const KViews &kv = *kvp;
     const int px = blockIdx.x * 64 + threadIdx.x;
-    const int py = blockIdx.y * 4 + threadIdx.y;
-    if (px >= kv.W || py >= kv.H) return;
+    const int py = (st.y0 / 4 + (int)blockIdx.y) * 4 + threadIdx.y;
+    if (px >= kv.W || py < st.y0 || py >= st.y1) return;
     const int c = (px + py) & 1;
     const int ci = cs_index(kv, px, py);
     float4 h = st.plane[c][ci];
@@ -1567,9 +1568,9 @@ __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp
 __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, KState st, int colour) {
     const KViews &kv = *kvp;
     const int k = blockIdx.x * 64 + threadIdx.x;
-    const int py = blockIdx.y * 4 + threadIdx.y;
+    const int py = (st.y0 / 4 + (int)blockIdx.y) * 4 + threadIdx.y;
     const int width = kv.W, height = kv.H;
-    if (py >= kv.sweep_rows) return;
+    if (py < st.y0 || py >= st.y1 || py >= kv.sweep_rows) return;
     const int px = 2 * k + ((py + colour) & 1);
     if (px >= width) return;
     float4 *ph = st.rm_plane;
@@ -1859,37 +1860,48 @@ static int ns_bucket(int nsrc) {
     }
 #endif
 
-static dim3 cs_grid(const KViews &kv, int colours) {
-    return dim3((kv.Wh + kBX - 1) / kBX, (kv.H + kBY - 1) / kBY, colours);
+// Colour-split grid over image rows [st.y0, st.y1): whole blocks of kBY
+// rows from the block row holding y0 (the kernels skip rows outside).
+static dim3 cs_grid(const KViews &kv, const KState &st, int colours) {
+    const int by0 = st.y0 / kBY;
+    return dim3((kv.Wh + kBX - 1) / kBX, (st.y1 - by0 * kBY + kBY - 1) / kBY, colours);
+}
+// 64 x 4 grid over rows [st.y0, st.y1) and `cols` columns
+static dim3 row_grid(int cols, const KState &st) {
+    return dim3((cols + 63) / 64, (st.y1 - (st.y0 / 4) * 4 + 3) / 4);
 }
 
 hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
-    ACMMP_LAUNCH_NS(k_init, cs_grid(h_kv, 2), dim3(kBX, kBY), stream, d_kv, st);
+    if (st.y1 <= st.y0) return hipSuccess;
+    ACMMP_LAUNCH_NS(k_init, cs_grid(h_kv, st, 2), dim3(kBX, kBY), stream, d_kv, st);
     return hipGetLastError();
 }
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
-    ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+    if (st.y1 <= st.y0) return hipSuccess;
+    ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, st, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
     return hipGetLastError();
 }
 
 hipError_t launch_finalize(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
-    dim3 block(64, 4), grid((h_kv.W + 63) / 64, (h_kv.H + 3) / 4);
-    k_finalize<<<grid, block, 0, stream>>>(d_kv, st);
+    if (st.y1 <= st.y0) return hipSuccess;
+    k_finalize<<<row_grid(h_kv.W, st), dim3(64, 4), 0, stream>>>(d_kv, st);
     return hipGetLastError();
 }
 
 hipError_t launch_filter(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour,
                          hipStream_t stream) {
-    dim3 block(64, 4), grid((h_kv.Wh + 63) / 64, (h_kv.H + 3) / 4);
-    k_filter<<<grid, block, 0, stream>>>(d_kv, st, colour);
+    if (st.y1 <= st.y0) return hipSuccess;
+    k_filter<<<row_grid(h_kv.Wh, st), dim3(64, 4), 0, stream>>>(d_kv, st, colour);
     return hipGetLastError();
 }
 
 hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float4 *planes, float *out,
                              float *out_init, uint32_t *out_views, hipStream_t stream) {
-    ACMMP_LAUNCH_NS(k_eval_costs, cs_grid(h_kv, 2), dim3(kBX, kBY), stream, d_kv, planes, out, out_init,
+    KState all{};
+    all.y1 = h_kv.H;
+    ACMMP_LAUNCH_NS(k_eval_costs, cs_grid(h_kv, all, 2), dim3(kBX, kBY), stream, d_kv, planes, out, out_init,
                     out_views);
     return hipGetLastError();
 }

@@ -351,6 +351,27 @@ class ACMMP:
     def synchronize(self):
         self._check(self._lib.acmmp_synchronize(self._ctx), "acmmp_synchronize")
 
+    def run_band(self, row_lo: int, row_hi: int, exchange):
+        """acmmp_run_patchmatch_band: this participant's rows [row_lo, row_hi)
+        of a row-band split RunPatchMatch; `exchange(halo: _abi.BandHalo)`
+        trades the halo rows after every half-sweep (acmmp_amd.band). A
+        Python exception in it fails the run and is re-raised here."""
+        err = []
+
+        def cb(_user, halo):
+            try:
+                exchange(halo.contents)
+                return 0
+            except BaseException as e:  # noqa: BLE001 — re-raised below
+                err.append(e)
+                return 1
+
+        fn = _abi.BandExchangeFn(cb)
+        rc = self._lib.acmmp_run_patchmatch_band(self._ctx, int(row_lo), int(row_hi), fn, None)
+        if err:
+            raise err[0]
+        self._check(rc, "acmmp_run_patchmatch_band")
+
     def set_timing(self, enable: bool = True):
         self._check(self._lib.acmmp_set_timing(self._ctx, int(enable)), "acmmp_set_timing")
 

@@ -276,6 +276,40 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx);
 /* Waits for all work enqueued on the engine's stream. */
 int acmmp_synchronize(acmmp_ctx *ctx);
 
+/* ---- Row-band split of ONE RunPatchMatch over several engines / ranks
+ * (SURVEY §5 "image-size scaling": the reference has no intra-image split).
+ * Each participant runs acmmp_run_patchmatch_band on the same inputs with
+ * its own rows [row_lo, row_hi) of the reference image (the bands tile
+ * 0..H). The sweeps compute only those rows; a pixel's CheckerboardPropagation
+ * reads neighbour state up to ACMMP_BAND_HALO rows away (the far searches,
+ * src/ACMMP.cu:819-826: 3 + 2 * 10 rows), so after every half-sweep the
+ * engine calls `exchange` with the colour just written: the participant
+ * must send its rows [send_*_lo, send_*_hi) of that colour's state to the
+ * band above / below and receive theirs into rows [recv_*_lo, recv_*_hi)
+ * (empty ranges where there is no neighbour). State rows are colour-split
+ * (Wh elements per pixel row: plane float4, cost float, selected-views
+ * u32). Initialisation runs on the band plus the halo rows (every pixel's
+ * start is a function of its own inputs: the halos start valid), depth /
+ * normal conversion and the two median filters on the band plus the rows the
+ * filters read. Results (acmmp_get_* / acmmp_export_results) are valid for
+ * rows [row_lo, row_hi) and bit-identical to acmmp_run_patchmatch's there.
+ * Synchronous: returns when the run is complete. */
+#define ACMMP_BAND_HALO 23
+typedef struct acmmp_band_halo {
+    int32_t colour;       /* checkerboard colour just written (0 black, 1 red) */
+    int32_t Wh;           /* state elements per pixel row */
+    void *plane;          /* float4 [H][Wh]: the colour's current planes (device) */
+    void *cost;           /* float  [H][Wh] */
+    void *sv;             /* u32    [H][Wh] */
+    void *stream;         /* the engine's hipStream_t: enqueue on it, or synchronise it first */
+    int32_t send_up_lo, send_up_hi;      /* own rows the band above reads */
+    int32_t send_down_lo, send_down_hi;  /* own rows the band below reads */
+    int32_t recv_up_lo, recv_up_hi;      /* rows of the band above this band reads */
+    int32_t recv_down_lo, recv_down_hi;  /* rows of the band below this band reads */
+} acmmp_band_halo;
+typedef int (*acmmp_band_exchange_fn)(void *user, const acmmp_band_halo *halo);
+int acmmp_run_patchmatch_band(acmmp_ctx *ctx, int row_lo, int row_hi, acmmp_band_exchange_fn exchange, void *user);
+
 /* Bulk getters replacing the per-pixel GetPlaneHypothesis(int)/GetCost(int)
  * loops (src/ACMMP.cpp:848-856, src/acmmp_definitions.cpp:287-295).
  * `n` = capacity in elements (float4 count / float count / u32 count). */

@@ -87,8 +87,8 @@ def main():
                         "t0 = time.perf_counter(); n = pipeline.run_fusion(%r, %r); "
                         "print(json.dumps({'points': n, 's': round(time.perf_counter() - t0, 2)}))"
                         % (ROOT, dense, dense + "/ACMMP_dist"))
-                r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
-                                   env=dict(os.environ, ACMMP_LIB=lib))
+                r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, check=True,
+                                   env=dict(os.environ, ACMMP_LIB=lib))  # stderr: ACMMP_HOST_TIMING lines
                 res = json.loads(r.stdout.strip().splitlines()[-1])
                 emit(step="fusion_of_distributed_maps", lib=os.path.basename(lib), points=res["points"], s=res["s"],
                      host_threads=int(_lib().acmmp_host_threads()))
