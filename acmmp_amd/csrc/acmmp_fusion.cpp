@@ -477,9 +477,9 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     // values, same sum order), then points are emitted and masks / used_list
     // updated. View i + 1's phase 1 runs while view i is walked.
     struct Hit {
-        int j;
-        uint32_t sp;
-        float ex;
+        uint32_t sp;  // source pixel (row-major index)
+        int32_t j;    // source slot
+        float ex;     // exp(-tmp_index)
     };
     struct ViewHits {
         std::vector<std::vector<Hit>> row;         // hits of row r, pixel order
@@ -524,7 +524,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     const float angle = get_angle(ref_normal, src_normal);
                     if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
                         const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                        h.push_back(Hit{j, (uint32_t)sp, std::exp(-tmp_index)});
+                        h.push_back(Hit{(uint32_t)sp, j, std::exp(-tmp_index)});
                     }
                 }
             }
@@ -544,19 +544,38 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     for (size_t i = 0; i < n; ++i) {
         const int W = cols[i], H = rows[i];
         const int num_ngb = problems[i].num_src_images;
-        std::vector<int> used_x(num_ngb, -1), used_y(num_ngb, -1);
-        std::vector<uint8_t> approved((size_t)W * H, 0);
+        std::vector<uint8_t> approved(write_debug_images ? (size_t)W * H : 0, 0);
         const auto t0 = now();
         pool.wait(job);
         const auto t1 = now();
         t_wait += secs(t0, t1);
         if (i + 1 < n) job = start_phase1(i + 1);
         const ViewHits &vh = vhits[i & 1];
+        // per source: its mask words; used_list as mask indices (-1 unset)
+        std::vector<uint64_t *> mw((size_t)std::max(num_ngb, 1));
+        for (int j = 0; j < num_ngb; ++j) mw[(size_t)j] = masks[(size_t)src_index[i][j]].w.data();
+        std::vector<int64_t> used_sp((size_t)std::max(num_ngb, 1), -1);
+        auto bit = [](const uint64_t *w, size_t k) -> bool {
+            return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
+        };
+        constexpr int kAhead = 6;  // pixels whose source mask words are prefetched ahead of the walk
         for (int r = 0; r < H; ++r) {
             const Hit *h = vh.row[(size_t)r].data();
+            const uint16_t *nhr = vh.nhit[(size_t)r].data();
+            const Hit *hpf = h;
+            int cpf = 0;
+            auto prefetch_to = [&](int upto) {
+                for (; cpf < W && cpf < upto; ++cpf) {
+                    const int n = nhr[cpf];
+                    if (n == 0xffff) continue;
+                    for (int k = 0; k < n; ++k) __builtin_prefetch(&mw[hpf[k].j][hpf[k].sp >> 6]);
+                    hpf += n;
+                }
+            };
             for (int c = 0; c < W; ++c) {
+                prefetch_to(c + 1 + kAhead);
                 const size_t pc = (size_t)r * W + c;
-                const int nh = vh.nhit[(size_t)r][(size_t)c];
+                const int nh = nhr[c];
                 if (nh == 0xffff) continue;
                 const Hit *hp = h;
                 h += nh;
@@ -565,10 +584,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 int num_consistent = 0;
                 float dynamic_consistency = 0;
                 for (int k = 0; k < nh; ++k) {
-                    const int s = src_index[i][hp[k].j];
-                    if (masks[s].get(hp[k].sp)) continue;
-                    used_x[hp[k].j] = (int)(hp[k].sp % (uint32_t)cols[s]);
-                    used_y[hp[k].j] = (int)(hp[k].sp / (uint32_t)cols[s]);
+                    if (bit(mw[hp[k].j], hp[k].sp)) continue;
+                    used_sp[hp[k].j] = hp[k].sp;
                     dynamic_consistency += hp[k].ex;
                     num_consistent++;
                 }
@@ -583,11 +600,15 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     cloud.push_back(p);
                     // used_list is not reset per pixel in the reference: stale entries apply too
                     for (int j = 0; j < num_ngb; ++j) {
-                        if (used_x[j] == -1) continue;
+                        const int64_t sp = used_sp[(size_t)j];
+                        if (sp < 0) continue;
                         const int s = src_index[i][j];
-                        masks[s].set((size_t)used_y[j] * cols[s] + used_x[j]);
-                        // `approved` is this view's W x H image indexed by source coordinates (:1030)
-                        if (used_y[j] < H && used_x[j] < W) approved[(size_t)used_y[j] * W + used_x[j]] = 255;
+                        masks[s].set((size_t)sp);
+                        if (write_debug_images) {
+                            // `approved` is this view's W x H image indexed by source coordinates (:1030)
+                            const int ux = (int)(sp % cols[s]), uy = (int)(sp / cols[s]);
+                            if (uy < H && ux < W) approved[(size_t)uy * W + ux] = 255;
+                        }
                     }
                 }
             }
