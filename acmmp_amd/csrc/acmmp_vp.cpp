@@ -35,12 +35,14 @@
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -92,10 +94,27 @@ void recv_all(int fd, void *p, size_t n) {
     char *c = static_cast<char *>(p);
     while (n) {
         const ssize_t k = ::recv(fd, c, n, 0);
+        if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
+            fail("exchange: no data from a peer within ACMMP_EXCHANGE_TIMEOUT (a rank failed or hangs)");
         if (k <= 0) fail("rendezvous recv failed (peer gone)");
         c += k;
         n -= (size_t)k;
     }
+}
+
+// Seconds a rank waits for its peers in one exchange step (a pass's
+// slowest rank included) before it gives up: ACMMP_EXCHANGE_TIMEOUT, 1800.
+int exchange_timeout_s() {
+    const char *to = std::getenv("ACMMP_EXCHANGE_TIMEOUT");
+    const int s = to && *to ? std::atoi(to) : 1800;
+    return s > 0 ? s : 1800;
+}
+
+void set_socket_timeout(int fd, int seconds) {
+    timeval tv{};
+    tv.tv_sec = seconds;
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
 }
 
 class Group {
@@ -127,12 +146,14 @@ class Group {
                 const int fd = ::accept(ls, nullptr, nullptr);
                 if (fd < 0) fail("rendezvous accept failed");
                 ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+                set_socket_timeout(fd, std::max(1, timeout_ms / 1000));  // the announcement
                 int32_t r = -1;
                 recv_all(fd, &r, sizeof r);
                 if (r <= 0 || r >= world || peers_[r] >= 0) fail("rendezvous: bad rank announcement");
                 peers_[r] = fd;
             }
             ::close(ls);
+            for (int k = 1; k < world; ++k) set_socket_timeout(peers_[k], exchange_timeout_s());
         } else {
             addrinfo hints{}, *res = nullptr;
             hints.ai_family = AF_INET;
@@ -152,6 +173,7 @@ class Group {
             if (fd < 0) fail("rendezvous: cannot connect to " + addr + ":" + std::to_string(port));
             const int one = 1;
             ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+            set_socket_timeout(fd, exchange_timeout_s());
             const int32_t r = rank;
             send_all(fd, &r, sizeof r);
             root_ = fd;
@@ -222,6 +244,8 @@ class Exchange {
         if (rccl_) {  // world 1 included: the same RCCL call as at 8 GPUs
             const ncclResult_t r = ncclAllGather(d_send, d_recv, count, ncclFloat32, comm_, stream_);
             if (r != ncclSuccess) fail(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+            wait_rccl();
+            return;
         } else if (g_.world == 1) {
             hip_check(hipMemcpyAsync(d_recv, d_send, count * sizeof(float), hipMemcpyDeviceToDevice, stream_),
                       "hipMemcpyAsync");
@@ -236,6 +260,32 @@ class Exchange {
     }
 
   private:
+    // the all-gather has finished, or the communicator reported an error /
+    // the peers did not arrive within ACMMP_EXCHANGE_TIMEOUT: then abort it
+    // (the peers' collectives fail too) and exit non-zero instead of blocking
+    void wait_rccl() {
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(exchange_timeout_s());
+        for (;;) {
+            const hipError_t q = hipStreamQuery(stream_);
+            if (q == hipSuccess) return;
+            if (q != hipErrorNotReady) hip_check(q, "ncclAllGather stream");
+            ncclResult_t async = ncclSuccess;
+            if (ncclCommGetAsyncError(comm_, &async) != ncclSuccess || async != ncclSuccess) {
+                abort_comm();
+                fail(std::string("ncclAllGather: ") + ncclGetErrorString(async));
+            }
+            if (std::chrono::steady_clock::now() > deadline) {
+                abort_comm();
+                fail("ncclAllGather: peers did not arrive within ACMMP_EXCHANGE_TIMEOUT");
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    void abort_comm() {
+        (void)ncclCommAbort(comm_);
+        comm_ = nullptr;
+    }
+
     Group &g_;
     bool rccl_;
     ncclComm_t comm_ = nullptr;
@@ -327,6 +377,9 @@ class Driver {
             acmmp_ctx *ctx = nullptr;
             acmmp_check(acmmp_create(o.device, &ctx), "acmmp_create");
             engines_.push_back(ctx);
+            hipStream_t cs = nullptr;
+            hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
+            copy_.push_back(cs);
         }
     }
 
@@ -334,6 +387,7 @@ class Driver {
         for (auto &t : writers_)
             if (t.joinable()) t.join();
         for (auto *e : engines_) acmmp_destroy(e);
+        for (auto cs : copy_) (void)hipStreamDestroy(cs);
         for (auto &kv : textures_) acmmp_texture_destroy(kv.second);
     }
 
@@ -560,7 +614,7 @@ class Driver {
     // the gathered depth map of problem i (previous pass)
     const float *gathered(int i) const { return gathered_in(recv_, i); }
 
-    void compute(acmmp_ctx *eng, const Task &t, ViewState &out) {
+    void compute(acmmp_ctx *eng, const Task &t, ViewState &out, hipStream_t cs) {
         const acmmp_problem &pr = problems_[(size_t)t.v];
         std::vector<int> ids = {pr.ref_image_id};
         for (int s = 0; s < pr.num_src_images; ++s) ids.push_back(pr.src_image_ids[s]);
@@ -597,10 +651,14 @@ class Driver {
             scaled = DevBuf(S * 4);
             // built on the device: the normals, then the 4th channel as a
             // strided copy (4 of every 16 bytes), as the Python driver does
-            hip_check(hipMemcpy(scaled.p, prev.planes.p, S * 4 * sizeof(float), hipMemcpyDeviceToDevice), "hipMemcpy");
-            hip_check(hipMemcpy2D(scaled.p + 3, 4 * sizeof(float), upsample ? prev.costs.p : prev.jbu.p, sizeof(float),
-                                  sizeof(float), S, hipMemcpyDeviceToDevice),
-                      "hipMemcpy2D");
+            // (device-to-device hipMemcpy does not wait for the copy, and the
+            // engine stream is non-blocking: copy on `cs` and wait for it)
+            hip_check(hipMemcpyAsync(scaled.p, prev.planes.p, S * 4 * sizeof(float), hipMemcpyDeviceToDevice, cs),
+                      "hipMemcpyAsync");
+            hip_check(hipMemcpy2DAsync(scaled.p + 3, 4 * sizeof(float), upsample ? prev.costs.p : prev.jbu.p,
+                                       sizeof(float), sizeof(float), S, hipMemcpyDeviceToDevice, cs),
+                      "hipMemcpy2DAsync");
+            hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
             acmmp_check(acmmp_set_hierarchy_inputs_device(eng, scaled.p, sw, sh, prev.jbu.p),
                         "acmmp_set_hierarchy_inputs_device", eng);
         }
@@ -656,7 +714,7 @@ class Driver {
         auto worker = [&](size_t e) {
             try {
                 hip_check(hipSetDevice(o_.device), "hipSetDevice");  // per thread: the output buffers go there
-                for (size_t k; (k = q++) < tasks.size();) compute(engines_[e], tasks[k], next[tasks[k].v]);
+                for (size_t k; (k = q++) < tasks.size();) compute(engines_[e], tasks[k], next[tasks[k].v], copy_[e]);
             } catch (const std::exception &ex) {
                 errs[e] = ex.what();
                 q = tasks.size();
@@ -704,9 +762,10 @@ class Driver {
             const acmmp_camera &c = cams_.at(id);
             const size_t P = (size_t)s.W * s.H;
             DevBuf d(P);  // the depth channel of the previous scale's planes
-            hip_check(hipMemcpy2D(d.p, sizeof(float), s.planes.p + 3, 4 * sizeof(float), sizeof(float), P,
-                                  hipMemcpyDeviceToDevice),
-                      "hipMemcpy2D");
+            hip_check(hipMemcpy2DAsync(d.p, sizeof(float), s.planes.p + 3, 4 * sizeof(float), sizeof(float), P,
+                                       hipMemcpyDeviceToDevice, copy_[0]),
+                      "hipMemcpy2DAsync");
+            hip_check(hipStreamSynchronize(copy_[0]), "hipStreamSynchronize");  // the JBU runs on its own stream
             s.jbu = DevBuf((size_t)c.width * c.height);
             int isc = 0;
             acmmp_check(acmmp_joint_bilateral_upsample_device(o_.device, images_.at(id).p, c.width, c.height, d.p, s.W,
@@ -726,6 +785,7 @@ class Driver {
     std::vector<std::vector<int>> assignment_;
     std::vector<int> mine_;
     std::vector<acmmp_ctx *> engines_;
+    std::vector<hipStream_t> copy_;  // per engine: the driver's device-to-device copies
     std::map<int, DevBuf> images_;
     std::map<int, acmmp_texture *> textures_;  // ~ the reference's texture objects, per image and scale
     std::map<int, acmmp_camera> cams_;
