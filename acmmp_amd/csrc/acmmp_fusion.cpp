@@ -401,6 +401,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     };
     const auto t_start = now();
     double t_wait = 0, t_walk = 0;
+    size_t n_live = 0, n_hits = 0, n_masked = 0;
     // views load independently (JPEG decode, two .dmb reads, optional mask)
     int load_rc = parallel_for((int)n, [&](int vi) -> int {
         const size_t i = (size_t)vi;
@@ -476,23 +477,33 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     // against the current masks and accumulated in ascending j (same exp
     // values, same sum order), then points are emitted and masks / used_list
     // updated. View i + 1's phase 1 runs while view i is walked.
-    struct Hit {
-        uint32_t sp;  // source pixel (row-major index)
-        int32_t j;    // source slot
-        float ex;     // exp(-tmp_index)
-    };
+    // A hit = (source slot j, source pixel sp) packed in 32 bits; its
+    // exp(-tmp_index) is kept beside it, and every live pixel's sum of them
+    // (ascending j, as the walk adds) is precomputed: the walk reads the
+    // per-hit values only for pixels where some hit became masked.
+    constexpr int kSpBits = 27;
     struct ViewHits {
-        std::vector<std::vector<Hit>> row;         // hits of row r, pixel order
+        std::vector<std::vector<uint32_t>> hit;    // hits of row r, pixel order: j << kSpBits | sp
+        std::vector<std::vector<float>> ex;        // their exp(-tmp_index)
         std::vector<std::vector<uint16_t>> nhit;   // hits per pixel; 0xffff = not live
+        std::vector<std::vector<float>> sum;       // per pixel: sum of its hits' ex, ascending j
     };
+    for (size_t i = 0; i < n; ++i)
+        if ((size_t)cols[i] * rows[i] > (size_t(1) << kSpBits) || problems[i].num_src_images > 32)
+            return ffail(ACMMP_ERR_ARG, "view %d: fusion supports images up to 2^27 pixels and 32 sources",
+                         problems[i].ref_image_id);
     auto phase1 = [&](size_t i, ViewHits &vh, int r) {
         const int W = cols[i];
         const int num_ngb = problems[i].num_src_images;
         const float depth_max = cameras[i].depth_max;
-        std::vector<Hit> &h = vh.row[(size_t)r];
+        std::vector<uint32_t> &h = vh.hit[(size_t)r];
+        std::vector<float> &hx = vh.ex[(size_t)r];
         std::vector<uint16_t> &nh = vh.nhit[(size_t)r];
+        std::vector<float> &sum = vh.sum[(size_t)r];
         h.clear();
+        hx.clear();
         nh.assign((size_t)W, 0xffff);
+        sum.assign((size_t)W, 0.0f);
         for (int c = 0; c < W; ++c) {
             const size_t pc = (size_t)r * W + c;
             if (masks[i].get(pc)) continue;
@@ -501,6 +512,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
             const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
             const size_t k0 = h.size();
+            float total = 0;
             for (int j = 0; j < num_ngb; ++j) {
                 const int s = src_index[i][j];
                 const int src_cols = cols[s], src_rows = rows[s];
@@ -524,18 +536,24 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     const float angle = get_angle(ref_normal, src_normal);
                     if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
                         const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                        h.push_back(Hit{(uint32_t)sp, j, std::exp(-tmp_index)});
+                        const float e = std::exp(-tmp_index);
+                        h.push_back((uint32_t)j << kSpBits | (uint32_t)sp);
+                        hx.push_back(e);
+                        total += e;
                     }
                 }
             }
             nh[(size_t)c] = (uint16_t)(h.size() - k0);
+            sum[(size_t)c] = total;
         }
     };
     std::vector<ViewHits> vhits(2);
     auto start_phase1 = [&](size_t i) {
         ViewHits &vh = vhits[i & 1];
-        vh.row.resize((size_t)rows[i]);
+        vh.hit.resize((size_t)rows[i]);
+        vh.ex.resize((size_t)rows[i]);
         vh.nhit.resize((size_t)rows[i]);
+        vh.sum.resize((size_t)rows[i]);
         return pool.submit(rows[i], [&, i](int r) { phase1(i, vhits[i & 1], r); });
     };
     std::vector<Point> cloud;
@@ -559,16 +577,19 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
         };
         constexpr int kAhead = 6;  // pixels whose source mask words are prefetched ahead of the walk
+        constexpr uint32_t kSpMask = (1u << kSpBits) - 1;
         for (int r = 0; r < H; ++r) {
-            const Hit *h = vh.row[(size_t)r].data();
+            const uint32_t *h = vh.hit[(size_t)r].data();
+            const float *hx = vh.ex[(size_t)r].data();
             const uint16_t *nhr = vh.nhit[(size_t)r].data();
-            const Hit *hpf = h;
+            const float *sumr = vh.sum[(size_t)r].data();
+            const uint32_t *hpf = h;
             int cpf = 0;
             auto prefetch_to = [&](int upto) {
                 for (; cpf < W && cpf < upto; ++cpf) {
                     const int n = nhr[cpf];
                     if (n == 0xffff) continue;
-                    for (int k = 0; k < n; ++k) __builtin_prefetch(&mw[hpf[k].j][hpf[k].sp >> 6]);
+                    for (int k = 0; k < n; ++k) __builtin_prefetch(&mw[hpf[k] >> kSpBits][(hpf[k] & kSpMask) >> 6]);
                     hpf += n;
                 }
             };
@@ -577,17 +598,31 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 const size_t pc = (size_t)r * W + c;
                 const int nh = nhr[c];
                 if (nh == 0xffff) continue;
-                const Hit *hp = h;
+                const uint32_t *hp = h;
+                const float *hxp = hx;
                 h += nh;
+                hx += nh;
                 // masks[i] changes during view i only if i is its own source
                 if (masks[i].get(pc)) continue;
                 int num_consistent = 0;
-                float dynamic_consistency = 0;
+                bool masked = false;
                 for (int k = 0; k < nh; ++k) {
-                    if (bit(mw[hp[k].j], hp[k].sp)) continue;
-                    used_sp[hp[k].j] = hp[k].sp;
-                    dynamic_consistency += hp[k].ex;
+                    const uint32_t j = hp[k] >> kSpBits, sp = hp[k] & kSpMask;
+                    if (bit(mw[j], sp)) {
+                        masked = true;
+                        continue;
+                    }
+                    used_sp[j] = sp;
                     num_consistent++;
+                }
+                float dynamic_consistency = sumr[c];
+                n_live++;
+                n_hits += (size_t)nh;
+                n_masked += masked;
+                if (masked) {  // re-add the unmasked ones, ascending j
+                    dynamic_consistency = 0;
+                    for (int k = 0; k < nh; ++k)
+                        if (!bit(mw[hp[k] >> kSpBits], hp[k] & kSpMask)) dynamic_consistency += hxp[k];
                 }
                 if (num_consistent >= con_num_thresh && (dynamic_consistency > consistency_scalar * num_consistent)) {
                     const float ref_depth = depths[i][pc];
@@ -626,8 +661,11 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     const auto t_walked = now();
     const int rc = store_ply(out + "/ACMMP_model.ply", cloud);
     if (timing)
-        std::fprintf(stderr, "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d\n",
-                     secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), acmmp_host_threads());
+        std::fprintf(stderr,
+                     "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d "
+                     "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu\n",
+                     secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), acmmp_host_threads(), n_live,
+                     n_hits, n_masked, cloud.size());
     return rc;
 }
 
