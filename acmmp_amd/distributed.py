@@ -49,6 +49,29 @@ def lpt_assign(costs: list, world: int) -> list:
     return [sorted(o) for o in out]
 
 
+def plan_views(costs: list, world: int, split_tail: bool) -> tuple:
+    """The pass's view placement: (assignment, split). Without split_tail,
+    assignment = lpt_assign and split = []. With it, the V mod world
+    cheapest views — the tail that leaves some ranks one view longer than
+    the others — are split into row bands over ALL ranks (acmmp_amd.band,
+    bit-exact to the unsplit run) and the rest are LPT-assigned; each split
+    view still has one owner rank (least loaded first), which decodes its
+    image into the all-gathers and writes its .dmb files."""
+    n = len(costs)
+    r = n % world if split_tail and world > 1 else 0
+    order = sorted(range(n), key=lambda i: (-costs[i], i))
+    split = sorted(order[n - r:]) if r else []
+    whole = [v for v in range(n) if v not in set(split)]
+    sub = lpt_assign([costs[v] for v in whole], world)
+    assignment = [[whole[k] for k in a] for a in sub]
+    load = [sum(costs[v] for v in a) for a in assignment]
+    for v in split:
+        k = min(range(world), key=lambda q: (load[q], q))
+        assignment[k].append(v)
+        load[k] += costs[v]
+    return [sorted(a) for a in assignment], split
+
+
 class DepthExchange:
     """All-gather of per-view depth maps of different sizes over a padded
     [world * slots, Hmax, Wmax] buffer with all_gather_into_tensor (RCCL has
@@ -148,17 +171,7 @@ def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
     H, W = ref.shape
     planes = torch.empty((H, W, 4), dtype=torch.float32, device=ref.device)
     costs = torch.empty((H, W), dtype=torch.float32, device=ref.device)
-    eng.set_params(_view_params(t))
-    if t.textures is not None:
-        eng.set_images_textures(t.cams, t.textures)
-    else:
-        eng.set_images_device(t.cams, [im.data_ptr() for im in t.images], [im.stride(0) for im in t.images])
-    if t.geom:
-        eng.set_depth_maps_device([d.data_ptr() for d in t.depths], [d.stride(0) for d in t.depths])
-        eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
-    if t.hierarchy:
-        scaled, up = t.hier_inputs
-        eng.set_hierarchy_inputs_device(scaled.data_ptr(), scaled.shape[1], scaled.shape[0], up.data_ptr())
+    engine_setup(t, eng)
     gpu_ms = 0.0
     eng.run_async()
     if t.planar:
@@ -170,6 +183,23 @@ def engine_compute(t: ViewTask, eng: ACMMP) -> ViewResult:
     eng.synchronize()
     gpu_ms += _run_ms(eng)
     return ViewResult(planes, costs, {"gpu_ms": gpu_ms})
+
+
+def engine_setup(t: ViewTask, eng: ACMMP):
+    """ProcessProblem's inputs for one view on an engine (parameters, images,
+    and per pass kind the previous state, source depth maps and hierarchy
+    inputs), borrowed from HBM."""
+    eng.set_params(_view_params(t))
+    if t.textures is not None:
+        eng.set_images_textures(t.cams, t.textures)
+    else:
+        eng.set_images_device(t.cams, [im.data_ptr() for im in t.images], [im.stride(0) for im in t.images])
+    if t.geom:
+        eng.set_depth_maps_device([d.data_ptr() for d in t.depths], [d.stride(0) for d in t.depths])
+        eng.set_plane_hypotheses_device(t.state[0].data_ptr(), t.state[1].data_ptr())
+    if t.hierarchy:
+        scaled, up = t.hier_inputs
+        eng.set_hierarchy_inputs_device(scaled.data_ptr(), scaled.shape[1], scaled.shape[0], up.data_ptr())
 
 
 def _run_ms(eng: ACMMP) -> float:
@@ -207,7 +237,7 @@ class ViewParallelPipeline:
                  max_iterations: int = 0, geom_iterations: int = 2, group=None,
                  compute: Optional[Callable] = None, jbu: Optional[Callable] = None, write_outputs: bool = True,
                  comm_device: Optional[torch.device] = None, tensor_device: Optional[torch.device] = None,
-                 concurrent_views: int = 2, timing: bool = False):
+                 concurrent_views: int = 2, timing: bool = False, split_tail: bool = True):
         self.dense = dense_folder
         self.output_folder = dense_folder + output_dir
         self.device = device
@@ -248,8 +278,13 @@ class ViewParallelPipeline:
         for p in self.problems:
             w, h = aio.image_size(self._image_path(p.ref_image_id))
             costs.append(float(w * h * max(p.num_src_images, 1)))
-        self.assignment = lpt_assign(costs, self.world)
-        self.mine = self.assignment[self.rank]
+        # the tail views are split in row bands over all ranks (engine runs
+        # only: the injected CPU stand-ins compute whole views)
+        self.split_tail = bool(split_tail) and self.world > 1 and self.compute is engine_compute
+        self.assignment, self.split = plan_views(costs, self.world, self.split_tail)
+        self._split_checked = False
+        self.owned = self.assignment[self.rank]                  # decoded, gathered and written here
+        self.mine = [v for v in self.owned if v not in self.split]  # computed whole here
         self.state = {}     # own views: problem index -> ViewResult (latest pass)
         self.depths = {}    # every view: problem index -> depth tensor view (previous pass, gathered)
         self.pass_index = 0
@@ -270,8 +305,10 @@ class ViewParallelPipeline:
         hands every rank all of them; the cameras come from the headers."""
         import ctypes as C
         lib = _abi.load_library()
+        if not self._split_checked:
+            self._check_split()
         need = set()
-        for v in self.mine:
+        for v in self.mine + self.split:
             p = self.problems[v]
             need.add(p.ref_image_id)
             need.update(p.sources)
@@ -297,12 +334,12 @@ class ViewParallelPipeline:
 
         from concurrent.futures import ThreadPoolExecutor
         order = sorted(need)
-        own = [self.problems[v].ref_image_id for v in self.mine]
+        own = [self.problems[v].ref_image_id for v in self.owned]
         work = [(i, False) for i in order] + [(i, True) for i in own]
         with ThreadPoolExecutor(max_workers=max(1, min(lib.acmmp_host_threads(), len(work)))) as ex:
             loaded = list(ex.map(load, work))  # re-raises the first failure in id order
         self.cams = {i: cam for i, (_, cam) in zip(order, loaded[:len(order)])}
-        mine_imgs = {v: torch.from_numpy(img) for v, (img, _) in zip(self.mine, loaded[len(order):])}
+        mine_imgs = {v: torch.from_numpy(img) for v, (img, _) in zip(self.owned, loaded[len(order):])}
         shapes = self._shapes()
         for v, img in mine_imgs.items():
             if tuple(img.shape) != shapes[v]:
@@ -318,6 +355,16 @@ class ViewParallelPipeline:
         if self.compute is engine_compute and self.tdev.type == "cuda":
             from .engine import Texture
             self.textures = {i: Texture.of(im, self.device) for i, im in self.images.items()}
+
+    def _check_split(self):
+        """A view is split only if every band holds the 23-row halo at the
+        coarsest scale (this first load's shapes; later scales are larger);
+        otherwise its owner computes it whole."""
+        self._split_checked = True
+        shapes = self._shapes()
+        keep = [v for v in self.split if shapes[v][0] >= self.world * _abi.BAND_HALO]
+        self.split = keep
+        self.mine = [v for v in self.owned if v not in keep]
 
     @contextmanager
     def _timed(self, name: str):
@@ -355,33 +402,50 @@ class ViewParallelPipeline:
                 e.timing_on = self.timing
         return self.pool.map(lambda eng, t: self.compute(t, eng), tasks)
 
+    def _task(self, v: int, geom: bool, planar: bool, hierarchy: bool, multi: bool) -> ViewTask:
+        p = self.problems[v]
+        ids = [p.ref_image_id] + p.sources
+        t = ViewTask(index=v, ref_id=p.ref_image_id, ids=ids, cams=[self.cams[i] for i in ids],
+                     images=[self.images[i] for i in ids],
+                     textures=[self.textures[i] for i in ids] if self.textures else None,
+                     geom=geom, planar=planar, hierarchy=hierarchy,
+                     multi=multi, seed_lo=self.seed + p.ref_image_id, seed_hi=self.pass_index,
+                     max_iterations=self.max_iterations)
+        if geom:
+            t.depths = [self.depths[self.index_of[i]] for i in ids]
+            prev = self.state[v]
+            t.state = (prev.planes, prev.costs)
+        if hierarchy:
+            t_h = time.perf_counter()
+            prev = self.state[v]
+            H, W = t.images[0].shape
+            up = prev.extra["jbu_depth"]
+            sh, sw = prev.costs.shape
+            upsample = sw != H or sh != W  # src/ACMMP.cpp:766, rows/cols swap included
+            w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
+            scaled = torch.cat([prev.planes[..., :3], w[..., None]], -1).contiguous()
+            t.hier_inputs = (scaled, up.contiguous())
+            self.phase_s["hier_inputs"] += time.perf_counter() - t_h
+        return t
+
+    def _run_split(self, t: ViewTask) -> ViewResult:
+        """One view's pass split in row bands over every rank of the group
+        (acmmp_amd.band): the halos travel after every half-sweep (RCCL P2P,
+        or gloo), the bands are all-gathered, so every rank holds the view's
+        full state afterwards — bit-identical to the unsplit run."""
+        from .band import bands, run_split
+        if self.pool is None:
+            self._map([])
+        eng = self.pool.engines[0]
+        engine_setup(t, eng)
+        members = [dist.get_global_rank(self.group, k) if self.group is not None else k for k in range(self.world)]
+        H = t.images[0].shape[0]
+        planes, costs = run_split(eng, bands(H, self.world), members, self.rank, self.tdev, self.cdev, self.group,
+                                  planar_prior=t.planar)
+        return ViewResult(planes, costs, {})
+
     def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
-        tasks = []
-        for v in self.mine:
-            p = self.problems[v]
-            ids = [p.ref_image_id] + p.sources
-            t = ViewTask(index=v, ref_id=p.ref_image_id, ids=ids, cams=[self.cams[i] for i in ids],
-                         images=[self.images[i] for i in ids],
-                         textures=[self.textures[i] for i in ids] if self.textures else None,
-                         geom=geom, planar=planar, hierarchy=hierarchy,
-                         multi=multi, seed_lo=self.seed + p.ref_image_id, seed_hi=self.pass_index,
-                         max_iterations=self.max_iterations)
-            if geom:
-                t.depths = [self.depths[self.index_of[i]] for i in ids]
-                prev = self.state[v]
-                t.state = (prev.planes, prev.costs)
-            if hierarchy:
-                t_h = time.perf_counter()
-                prev = self.state[v]
-                H, W = t.images[0].shape
-                up = prev.extra["jbu_depth"]
-                sh, sw = prev.costs.shape
-                upsample = sw != H or sh != W  # src/ACMMP.cpp:766, rows/cols swap included
-                w = prev.costs if upsample else up.reshape(-1)[: sh * sw].reshape(sh, sw)
-                scaled = torch.cat([prev.planes[..., :3], w[..., None]], -1).contiguous()
-                t.hier_inputs = (scaled, up.contiguous())
-                self.phase_s["hier_inputs"] += time.perf_counter() - t_h
-            tasks.append(t)
+        tasks = [self._task(v, geom, planar, hierarchy, multi) for v in self.mine]
         with self._timed("compute"):
             self._sync()
             results = self._map(tasks)
@@ -393,6 +457,17 @@ class ViewParallelPipeline:
             local[v] = res.planes[..., 3]
             if self.write_outputs:
                 self._write(t.ref_id, res, geom)
+        # the tail views, every rank on a band of each
+        for v in self.split:
+            with self._timed("split_compute"):
+                t = self._task(v, geom, planar, hierarchy, multi)
+                self._sync()
+                res = self._run_split(t)
+            self.state[v] = res
+            if v in self.owned:
+                local[v] = res.planes[..., 3]
+                if self.write_outputs:
+                    self._write(t.ref_id, res, geom)
         with self._timed("exchange"):
             self.depths = exchange.gather(self.rank, local)
         self.pass_index += 1
@@ -455,7 +530,7 @@ class ViewParallelPipeline:
                     self.run_pass(False, True, False, False, exchange)
                 else:
                     with self._timed("jbu"):
-                        for v in self.mine:  # JointBilateralUpsampling, resident
+                        for v in self.mine + self.split:  # JointBilateralUpsampling, resident (split: on every rank)
                             p = self.problems[v]
                             img = self.images[p.ref_image_id]
                             up, isc = self.jbu(img, self.state[v].planes[..., 3])

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 
 from acmmp_amd import io as aio
 from acmmp_amd import scene
-from acmmp_amd.distributed import DepthExchange, ViewParallelPipeline, ViewResult, lpt_assign
+from acmmp_amd.distributed import DepthExchange, ViewParallelPipeline, ViewResult, lpt_assign, plan_views
 
 
 def _free_port():
@@ -31,6 +31,21 @@ def test_lpt_assign():
     a = lpt_assign([3.0, 2.0, 2.0, 1.0, 1.0, 1.0, 4.0], 3)
     assert sorted(v for r in a for v in r) == list(range(7))
     assert lpt_assign([1, 2], 4)[2:] == [[], []]
+
+
+def test_plan_views_split_tail():
+    """cfg4 at 8 ranks: 49 equal views -> 48 whole views, 6 per rank, and
+    the 49th split over all ranks, owned by rank 0."""
+    a, split = plan_views([1.0] * 49, 8, True)
+    assert split == [48]
+    assert [len(r) for r in a] == [7] + [6] * 7 and 48 in a[0]
+    assert sorted(v for r in a for v in r) == list(range(49))
+    # no tail: nothing split; split_tail off: plain LPT
+    assert plan_views([1.0] * 16, 8, True) == (lpt_assign([1.0] * 16, 8), [])
+    assert plan_views([1.0] * 49, 8, False) == (lpt_assign([1.0] * 49, 8), [])
+    # unequal views: the cheapest ones are split
+    a, split = plan_views([4.0, 1.0, 3.0, 2.0, 5.0], 2, True)
+    assert split == [1] and sorted(v for r in a for v in r) == list(range(5))
 
 
 def fake_compute(t, eng=None):

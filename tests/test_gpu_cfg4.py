@@ -70,8 +70,8 @@ def _check(out_folder, maps):
 @pytest.mark.timeout(900)
 def test_multi_scale_n21_python_driver_world2(ms_n21):
     d, maps = ms_n21
-    mine = _spawn(2, d, "gloo", "/C4PY")
-    assert sorted(mine[0] + mine[1]) == list(range(golden.NUM_VIEWS))
+    got = _spawn(2, d, "gloo", "/C4PY")
+    assert sorted(got[0][0] + got[1][0]) == list(range(golden.NUM_VIEWS))
     _check(d + "/C4PY", maps)
 
 

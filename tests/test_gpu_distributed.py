@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, dense, q, backend="gloo", out="/VP2"):
+def _worker(rank, world, port, dense, q, backend="gloo", out="/VP2", split_tail=True):
     if backend == "nccl":
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
@@ -37,9 +37,9 @@ def _worker(rank, world, port, dense, q, backend="gloo", out="/VP2"):
         comm = torch.device("cpu")
     try:
         pipe = ViewParallelPipeline(dense, out, device=0, tensor_device=torch.device("cuda", 0),
-                                    comm_device=comm)
+                                    comm_device=comm, split_tail=split_tail)
         pipe.run()
-        q.put((rank, pipe.mine))
+        q.put((rank, (pipe.owned, pipe.split)))
     finally:
         dist.destroy_process_group()
 
@@ -65,11 +65,13 @@ def test_world1_matches_oracle_jacobi(dense, jacobi_maps, concurrent):
     assert _compare(out, jacobi_maps) == 5 * 4
 
 
-def _spawn(world, dense, backend, out):
+def _spawn(world, dense, backend, out, split_tail=True):
+    """Runs the driver on `world` ranks; returns {rank: (owned views, split views)}."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, dense, q, backend, out)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dense, q, backend, out, split_tail))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -78,10 +80,15 @@ def _spawn(world, dense, backend, out):
     return dict(q.get(timeout=5) for _ in range(world))
 
 
-def test_world2_matches_oracle_jacobi(dense, jacobi_maps):
-    mine = _spawn(2, dense, "gloo", "/VP2")
-    assert sorted(mine[0] + mine[1]) == list(range(5)) and mine[0] and mine[1]
-    assert _compare(dense + "/VP2", jacobi_maps) == 5 * 4
+@pytest.mark.parametrize("split_tail", [False, True])
+def test_world2_matches_oracle_jacobi(dense, jacobi_maps, split_tail):
+    """5 views on 2 ranks: with split_tail the odd view is computed in two
+    row bands, one per rank, with the halos exchanged every half-sweep."""
+    out = "/VP2s" if split_tail else "/VP2"
+    got = _spawn(2, dense, "gloo", out, split_tail)
+    assert sorted(got[0][0] + got[1][0]) == list(range(5)) and got[0][0] and got[1][0]
+    assert got[0][1] == got[1][1] == ([4] if split_tail else [])
+    assert _compare(dense + out, jacobi_maps) == 5 * 4
 
 
 def test_world1_nccl_process_group_matches_oracle_jacobi(dense, jacobi_maps):
@@ -89,8 +96,8 @@ def test_world1_nccl_process_group_matches_oracle_jacobi(dense, jacobi_maps):
     all_gather_into_tensor on device buffers through RCCL after every pass,
     and the engines borrow the gathered maps (torch/RCCL stream
     ordering before the borrow)."""
-    mine = _spawn(1, dense, "nccl", "/VPN")
-    assert mine[0] == list(range(5))
+    got = _spawn(1, dense, "nccl", "/VPN")
+    assert got[0] == (list(range(5)), [])
     assert _compare(dense + "/VPN", jacobi_maps) == 5 * 4
 
 
@@ -103,10 +110,26 @@ def test_world2_multi_scale_matches_oracle_jacobi(tmp_path):
     d = str(tmp_path / "dense_ms")
     sc = scene.make_scene(num_views=4, width=1010, height=760)
     scene.write_dense_folder(sc, d, num_src=2)
-    mine = _spawn(2, d, "gloo", "/VPMS")
-    assert sorted(mine[0] + mine[1]) == list(range(4)) and mine[0] and mine[1]
+    got = _spawn(2, d, "gloo", "/VPMS")
+    assert sorted(got[0][0] + got[1][0]) == list(range(4)) and got[0][0] and got[1][0]
     maps = OraclePipeline(d).run_multi_scale("jacobi")
     assert _compare(d + "/VPMS", maps) == 4 * 4
+
+
+@pytest.mark.timeout(600)
+def test_world2_multi_scale_split_tail_matches_oracle_jacobi(tmp_path):
+    """The same schedule with 3 views on 2 ranks: the third view is split in
+    row bands over both ranks in every pass — photometric + planar prior
+    (prior built on both ranks from the gathered first run), geometric,
+    JBU + hierarchy — and every .dmb stays bit-exact to the oracle."""
+    d = str(tmp_path / "dense_ms3")
+    sc = scene.make_scene(num_views=3, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=2)
+    got = _spawn(2, d, "gloo", "/VPMS3")
+    assert got[0][1] == got[1][1] == [2]
+    assert sorted(got[0][0] + got[1][0]) == [0, 1, 2]
+    maps = OraclePipeline(d).run_multi_scale("jacobi")
+    assert _compare(d + "/VPMS3", maps) == 3 * 4
 
 
 def test_bench_under_torchrun_nccl_world1():
