@@ -573,6 +573,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::vector<uint64_t *> mw((size_t)std::max(num_ngb, 1));
         for (int j = 0; j < num_ngb; ++j) mw[(size_t)j] = masks[(size_t)src_index[i][j]].w.data();
         std::vector<int64_t> used_sp((size_t)std::max(num_ngb, 1), -1);
+        uint32_t dirty = 0;  // used_sp entries written since the last approval
         auto bit = [](const uint64_t *w, size_t k) -> bool {
             return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
         };
@@ -613,6 +614,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                         continue;
                     }
                     used_sp[j] = sp;
+                    dirty |= 1u << j;
                     num_consistent++;
                 }
                 float dynamic_consistency = sumr[c];
@@ -633,10 +635,13 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
                     p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
                     cloud.push_back(p);
-                    // used_list is not reset per pixel in the reference: stale entries apply too
-                    for (int j = 0; j < num_ngb; ++j) {
+                    // used_list is not reset per pixel in the reference: stale
+                    // entries apply too. An entry unchanged since the last
+                    // approval was set then (masks only go 0 -> 1), so only
+                    // the entries written since are applied.
+                    for (; dirty; dirty &= dirty - 1) {
+                        const int j = __builtin_ctz(dirty);
                         const int64_t sp = used_sp[(size_t)j];
-                        if (sp < 0) continue;
                         const int s = src_index[i][j];
                         masks[s].set((size_t)sp);
                         if (write_debug_images) {
@@ -732,6 +737,7 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         masks[i].assign((size_t)w * h, 0);
     }
     std::vector<Point> cloud;
+    if (getenv("FUS_RES")) cloud.reserve(6000000);
     Pool pool;
     // Same two-phase scheme as RunFusion: candidates (projection + metrics of
     // both maps) per band of rows on host threads against the current masks,
