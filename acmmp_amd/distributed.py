@@ -288,6 +288,7 @@ class ViewParallelPipeline:
         self.state = {}     # own views: problem index -> ViewResult (latest pass)
         self.depths = {}    # every view: problem index -> depth tensor view (previous pass, gathered)
         self.pass_index = 0
+        self.pass_log = []  # per pass: kind and wall seconds of its phases (tools/scale_sim.py)
 
     # ------------------------------------------------------------- inputs
     def _image_path(self, image_id: int) -> str:
@@ -446,9 +447,11 @@ class ViewParallelPipeline:
 
     def run_pass(self, geom: bool, planar: bool, hierarchy: bool, multi: bool, exchange: DepthExchange):
         tasks = [self._task(v, geom, planar, hierarchy, multi) for v in self.mine]
+        t0 = time.perf_counter()
         with self._timed("compute"):
             self._sync()
             results = self._map(tasks)
+        t1 = time.perf_counter()
         local = {}
         for t, res in zip(tasks, results):  # in view order, as the sequential loop
             v = t.index
@@ -468,8 +471,13 @@ class ViewParallelPipeline:
                 local[v] = res.planes[..., 3]
                 if self.write_outputs:
                     self._write(t.ref_id, res, geom)
+        t2 = time.perf_counter()
         with self._timed("exchange"):
             self.depths = exchange.gather(self.rank, local)
+        self.pass_log.append({"pass": self.pass_index, "geom": geom, "planar": planar, "hierarchy": hierarchy,
+                              "multi": multi, "views": len(self.mine), "split_views": len(self.split),
+                              "shape": list(tasks[0].images[0].shape) if tasks else None,
+                              "compute_s": t1 - t0, "split_s": t2 - t1, "exchange_s": time.perf_counter() - t2})
         self.pass_index += 1
 
     def _write(self, ref_id: int, res: ViewResult, geom: bool):

@@ -42,18 +42,29 @@ from acmmp_amd import pipeline  # noqa: E402
 from acmmp_amd.distributed import ViewParallelPipeline  # noqa: E402
 from acmmp_amd import load_library as _lib  # noqa: E402
 
-V = int(sys.argv[1]) if len(sys.argv) > 1 else 49
-W = int(sys.argv[2]) if len(sys.argv) > 2 else 1600
-H = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
-NSRC = int(sys.argv[4]) if len(sys.argv) > 4 else 20
-STEPS = set((sys.argv[5] if len(sys.argv) > 5 else "distributed,cli,fusion").split(","))
+_argv = sys.argv if __name__ == "__main__" else []
+V = int(_argv[1]) if len(_argv) > 1 else 49
+W = int(_argv[2]) if len(_argv) > 2 else 1600
+H = int(_argv[3]) if len(_argv) > 3 else 1200
+NSRC = int(_argv[4]) if len(_argv) > 4 else 20
+STEPS = set((_argv[5] if len(_argv) > 5 else "distributed,cli,fusion").split(","))
 
 
 def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def main():
+def cgroup_cpu_stat() -> dict:
+    """cgroup v2 cpu.stat counters (usage / throttling), {} if unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f if line.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
+def write_cfg4_dense(V, W, H, NSRC):
+    """The synthetic cfg4-shaped dense folder (rendered on cuda:0); returns (tmp, dense)."""
     dev = torch.device("cuda", 0)
     setup = scene.scene_setup(num_views=V, width=W, height=H, arc_deg=float(os.environ.get("ACMMP_ARC_DEG", "1.8")))
     views = []
@@ -65,9 +76,21 @@ def main():
     sc = scene.Scene(views=views, pairs=setup.pairs)
     tmp = tempfile.mkdtemp(prefix="acmmp_cfg4_")
     dense = os.path.join(tmp, "dense")
-    t0 = time.perf_counter()
     scene.write_dense_folder(sc, dense, num_src=NSRC)
+    return tmp, dense
+
+
+def main():
+    t0 = time.perf_counter()
+    tmp, dense = write_cfg4_dense(V, W, H, NSRC)
     emit(step="write_dense", views=V, width=W, height=H, nsrc=NSRC, s=round(time.perf_counter() - t0, 2))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            cpu_max = f.read().strip()
+    except OSError:
+        cpu_max = None
+    emit(step="host", cgroup_cpu_max=cpu_max, affinity_cpus=len(os.sched_getaffinity(0)),
+         host_threads=int(_lib().acmmp_host_threads()))
 
     if "distributed" in STEPS:
         t0 = time.perf_counter()
@@ -81,17 +104,29 @@ def main():
              gpu_runpatchmatch_s=round(pipe.gpu_ms / 1e3, 2),
              phases_s={k: round(v, 2) for k, v in sorted(pipe.phase_s.items())})
         if "fusion_dist" in STEPS:
+            # per library (ACMMP_FUSION_LIBS) and host-thread count
+            # (ACMMP_FUSION_THREADS, default the library's own budget), one
+            # subprocess each; the cgroup's CPU throttling over the call is
+            # reported beside the time
+            threads = [t for t in os.environ.get("ACMMP_FUSION_THREADS", "").split(",") if t]
             for lib in os.environ.get("ACMMP_FUSION_LIBS", os.path.join(ROOT, "acmmp_amd", "lib",
                                                                          "libacmmp_amd.so")).split(","):
-                code = ("import sys, time, json; sys.path.insert(0, %r); from acmmp_amd import pipeline; "
-                        "t0 = time.perf_counter(); n = pipeline.run_fusion(%r, %r); "
-                        "print(json.dumps({'points': n, 's': round(time.perf_counter() - t0, 2)}))"
-                        % (ROOT, dense, dense + "/ACMMP_dist"))
-                r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, check=True,
-                                   env=dict(os.environ, ACMMP_LIB=lib))  # stderr: ACMMP_HOST_TIMING lines
-                res = json.loads(r.stdout.strip().splitlines()[-1])
-                emit(step="fusion_of_distributed_maps", lib=os.path.basename(lib), points=res["points"], s=res["s"],
-                     host_threads=int(_lib().acmmp_host_threads()))
+                for nt in threads or [None]:
+                    code = ("import sys, time, json; sys.path.insert(0, %r); from acmmp_amd import pipeline; "
+                            "t0 = time.perf_counter(); n = pipeline.run_fusion(%r, %r); "
+                            "print(json.dumps({'points': n, 's': round(time.perf_counter() - t0, 2)}))"
+                            % (ROOT, dense, dense + "/ACMMP_dist"))
+                    env = dict(os.environ, ACMMP_LIB=lib)
+                    if nt:
+                        env["ACMMP_HOST_THREADS"] = nt
+                    c0 = cgroup_cpu_stat()
+                    r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, check=True,
+                                       env=env)  # stderr: ACMMP_HOST_TIMING lines
+                    c1 = cgroup_cpu_stat()
+                    res = json.loads(r.stdout.strip().splitlines()[-1])
+                    emit(step="fusion_of_distributed_maps", lib=os.path.basename(lib), points=res["points"],
+                         s=res["s"], host_threads=int(nt) if nt else int(_lib().acmmp_host_threads()),
+                         cgroup_delta={k: c1[k] - c0.get(k, 0) for k in c1})
         shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
     if "cli_vp" in STEPS:  # the C++ view-parallel driver, world 1 through RCCL
         cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
