@@ -409,6 +409,16 @@ static float ComputeBilateralWeight(const float xd, const float yd, const float 
     return dm_expf(-spatial / (2.0f * ss * ss) - color / (2.0f * sc * sc));
 }
 
+/* Pin P3 is inferred, not measured: no reference output pins it (DESIGN.md
+ * §2, "parity unpinned"). The r01 form — every product and moment rounded
+ * separately, `sum += a * b` and `sum_xy * inv - m_x * m_y` unfused — stays
+ * selectable in the oracle (only) for comparison against reference outputs
+ * should any become available: acmmp_oracle_set_p3_fused(0). The product
+ * kernels implement the fused form only. */
+static int g_p3_fused = 1;
+void acmmp_oracle_set_p3_fused(int fused) { g_p3_fused = fused != 0; }
+int acmmp_oracle_p3_fused(void) { return g_p3_fused; }
+
 /* ComputeBilateralNCC (src/ACMMP.cu:360-432) with pins P1-P3. */
 static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const f4 h) {
     const acmmp_params *prm = S->prm;
@@ -439,11 +449,19 @@ static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const 
              * reference's --use_fast_math) fuses every `sum += a * b` here */
             const float wr = w * ref_pix;
             const float ws = w * src_pix;
-            r_ref = dm_fma(w, ref_pix, r_ref);
-            r_rr = dm_fma(wr, ref_pix, r_rr);
-            r_src = dm_fma(w, src_pix, r_src);
-            r_ss = dm_fma(ws, src_pix, r_ss);
-            r_rs = dm_fma(wr, src_pix, r_rs);
+            if (g_p3_fused) {
+                r_ref = dm_fma(w, ref_pix, r_ref);
+                r_rr = dm_fma(wr, ref_pix, r_rr);
+                r_src = dm_fma(w, src_pix, r_src);
+                r_ss = dm_fma(ws, src_pix, r_ss);
+                r_rs = dm_fma(wr, src_pix, r_rs);
+            } else { /* r01: each product rounded, then added */
+                r_ref += wr;
+                r_rr += wr * ref_pix;
+                r_src += ws;
+                r_ss += ws * src_pix;
+                r_rs += wr * src_pix;
+            }
             r_w += w;
         }
         sum_ref += r_ref;
@@ -460,11 +478,14 @@ static float ComputeBilateralNCC(const orc_state *S, int src, const i2 p, const 
      * first operand) into fma(sum_xy, inv, -(m_x * m_y)). On a flat patch this
      * leaves var, covar as independent residuals instead of three equal ones,
      * which decides the kMinVar test and the cost there. */
-    const float var_ref = dm_fma(sum_ref_ref, inv, -(sum_ref * sum_ref));
-    const float var_src = dm_fma(sum_src_src, inv, -(sum_src * sum_src));
+    const float var_ref = g_p3_fused ? dm_fma(sum_ref_ref, inv, -(sum_ref * sum_ref))
+                                     : sum_ref_ref * inv - sum_ref * sum_ref;
+    const float var_src = g_p3_fused ? dm_fma(sum_src_src, inv, -(sum_src * sum_src))
+                                     : sum_src_src * inv - sum_src * sum_src;
     const float kMinVar = 1e-5f;
     if (var_ref < kMinVar || var_src < kMinVar) return cost_max;
-    const float covar = dm_fma(sum_ref_src, inv, -(sum_ref * sum_src));
+    const float covar = g_p3_fused ? dm_fma(sum_ref_src, inv, -(sum_ref * sum_src))
+                                   : sum_ref_src * inv - sum_ref * sum_src;
     const float var_rs = dm_sqrt(var_ref * var_src);
     float c = 1.0f - covar / var_rs;
     c = (c < cost_max) ? c : cost_max;   /* min(cost_max, .) : NaN -> cost_max */

@@ -73,10 +73,26 @@ def _load():
     lib.acmmp_oracle_prior_plane_estimate.restype = None
     lib.acmmp_oracle_prior_plane_estimate.argtypes = [C.POINTER(C.c_uint16), C.c_int, C.c_int, C.c_int,
                                                       C.POINTER(C.c_uint16), C.c_int, CAM, C.c_int, C.c_int, FP]
+    lib.acmmp_oracle_set_p3_fused.restype = None
+    lib.acmmp_oracle_set_p3_fused.argtypes = [C.c_int]
+    lib.acmmp_oracle_p3_fused.restype = C.c_int
     lib.acmmp_oracle_jbu.restype = C.c_int
     lib.acmmp_oracle_jbu.argtypes = [FP, C.c_int, C.c_int, FP, C.c_int, C.c_int, FP]
     _lib = lib
     return lib
+
+
+class p3_unfused:
+    """Context manager: the oracle's NCC with r01's unfused P3 form (every
+    product and moment rounded separately) instead of the inferred nvcc
+    contraction the product pins; for comparisons only."""
+
+    def __enter__(self):
+        _load().acmmp_oracle_set_p3_fused(0)
+        return self
+
+    def __exit__(self, *exc):
+        _load().acmmp_oracle_set_p3_fused(1)
 
 
 def _f(a):

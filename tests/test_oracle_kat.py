@@ -380,3 +380,26 @@ def test_initial_cost_and_selected_views_aggregation():
             assert views[y, x] == m, (x, y, hex(views[y, x]), hex(m))
             n_mixed += 0 < (vec[y, x] < 2).sum() < 5
     assert n_mixed > 10  # partial-validity pixels exercise top_k = min(valid, 4)
+
+
+def test_p3_forms_selectable_and_differ_only_where_documented():
+    """Pin P3 is inferred (parity unpinned): the oracle keeps
+    r01's unfused form selectable. On a textured patch both forms give the
+    same NCC to rounding; on a flat mid-grey patch they part: the fused
+    moments leave independent residuals (here cost 0), the unfused ones
+    identical residuals below kMinVar (cost_max)."""
+    prm = default_params()
+    c = _cam()
+    pl = np.array([0, 0, -1, 30], np.float32)
+    tex = _texture(48, 64, 3)
+    src = (tex * 1.1 + 3).astype(np.float32)
+    fused = oracle.ncc(prm, c, c, tex, src, 30, 20, pl)
+    flat = np.full((48, 64), 77.0, np.float32)
+    flat_fused = oracle.ncc(prm, c, c, flat, flat, 30, 20, pl)
+    with oracle.p3_unfused():
+        unfused = oracle.ncc(prm, c, c, tex, src, 30, 20, pl)
+        flat_unfused = oracle.ncc(prm, c, c, flat, flat, 30, 20, pl)
+    assert abs(fused - unfused) < 1e-5
+    assert flat_fused == 0.0 and flat_unfused == 2.0
+    # the default is restored: the product's form
+    assert oracle.ncc(prm, c, c, flat, flat, 30, 20, pl) == 0.0
