@@ -16,6 +16,7 @@
 // arbitrary); a colour image whose size differs from its depth map is resized
 // with a float bilinear filter (cv::resize's 8-bit fixed-point path is
 // unpinned).
+#include <sched.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -100,6 +101,73 @@ float get_angle(const float *a, const float *b) {  // GetAngle
     return angle;
 }
 
+// RunFusion's threads kept on ONE last-level-cache domain (on a many-CCD
+// host a view's candidate lists, written by the pool, and the masks, written
+// by the walk, otherwise cross between L3s on every access; the walk, which
+// is sequential, measured ~1.4 s or 5-7 s for cfg4 depending on where the
+// scheduler happened to put the threads, profiles/r03_fusion_ab.jsonl):
+// the calling thread is confined to the physical core it runs on, the
+// workers to the rest of that core's L3 domain (within the allowed CPUs).
+// Restored when RunFusion returns. ACMMP_FUSION_PIN=0 turns it off.
+class CacheDomain {
+  public:
+    CacheDomain() {
+        if (const char *e = std::getenv("ACMMP_FUSION_PIN"))
+            if (std::atoi(e) == 0) return;
+        const int cpu = sched_getcpu();
+        if (cpu < 0 || sched_getaffinity(0, sizeof saved_, &saved_)) return;
+        cpu_set_t l3 = cpus_of(cpu, "cache/index3/shared_cpu_list"), core = cpus_of(cpu, "topology/thread_siblings_list");
+        CPU_AND(&l3, &l3, &saved_);
+        CPU_AND(&core, &core, &saved_);
+        if (!CPU_ISSET(cpu, &core)) return;
+        CPU_XOR(&workers_, &l3, &core);  // l3 without the walk's core
+        CPU_AND(&workers_, &workers_, &l3);
+        if (CPU_COUNT(&workers_) < 1 || CPU_EQUAL(&l3, &saved_)) return;  // one domain already
+        if (sched_setaffinity(0, sizeof core, &core)) return;
+        pinned_ = true;
+    }
+    ~CacheDomain() {
+        if (pinned_) (void)sched_setaffinity(0, sizeof saved_, &saved_);
+    }
+    bool pinned() const { return pinned_; }
+    // worker threads: confine themselves (0 = no limit)
+    int workers() const { return pinned_ ? CPU_COUNT(&workers_) : 0; }
+    void confine_worker() const {
+        if (pinned_) (void)sched_setaffinity(0, sizeof workers_, &workers_);
+    }
+
+  private:
+    static cpu_set_t cpus_of(int cpu, const char *what) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        char path[160];
+        std::snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
+        FILE *f = std::fopen(path, "r");
+        if (!f) return set;
+        char buf[4096];
+        const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+        std::fclose(f);
+        buf[n] = 0;
+        for (char *p = buf; *p;) {  // "a-b,c,..."
+            char *end = nullptr;
+            const long a = std::strtol(p, &end, 10);
+            if (end == p) break;
+            long b = a;
+            p = end;
+            if (*p == '-') {
+                b = std::strtol(p + 1, &end, 10);
+                p = end;
+            }
+            for (long k = a; k <= b && k < CPU_SETSIZE; ++k)
+                if (k >= 0) CPU_SET((int)k, &set);
+            while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+        }
+        return set;
+    }
+    cpu_set_t saved_{}, workers_{};
+    bool pinned_ = false;
+};
+
 // A persistent pool of acmmp_host_threads() - 1 workers: `submit` hands out
 // indices 0..n-1 of a job to whichever worker is free (dynamic rows), `wait`
 // blocks until a job is done. The caller's thread stays free for the
@@ -111,9 +179,14 @@ class Pool {
         int n = 0;
         std::atomic<int> next{0}, done{0};
     };
-    Pool() {
-        const int nw = std::max(1, acmmp_host_threads() - 1);
-        for (int t = 0; t < nw; ++t) workers_.emplace_back([this] { loop(); });
+    explicit Pool(const CacheDomain *dom = nullptr) {
+        int nw = std::max(1, acmmp_host_threads() - 1);
+        if (dom && dom->workers() > 0) nw = std::min(nw, dom->workers());
+        for (int t = 0; t < nw; ++t)
+            workers_.emplace_back([this, dom] {
+                if (dom) dom->confine_worker();
+                loop();
+            });
     }
     ~Pool() {
         {
@@ -393,7 +466,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     std::vector<int> rows(n), cols(n);
     std::map<int, int> image_id_2_index;
     for (size_t i = 0; i < n; ++i) image_id_2_index[problems[i].ref_image_id] = (int)i;
-    Pool pool;
     const bool timing = std::getenv("ACMMP_HOST_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -469,6 +541,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                              problems[i].ref_image_id);
             src_index[i].push_back(it->second);
         }
+    CacheDomain dom;  // after the loads, which use every allowed CPU
+    Pool pool(&dom);
     // Two phases per view, exact to the sequential loop: (1) on the pool,
     // every pixel's per-source projections and consistency tests against
     // the masks as they stand (masks only ever go 0 -> 1, so a source or
@@ -577,7 +651,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         auto bit = [](const uint64_t *w, size_t k) -> bool {
             return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
         };
-        constexpr int kAhead = 6;  // pixels whose source mask words are prefetched ahead of the walk
+        static const int kAhead = std::getenv("ACMMP_FUS_AHEAD") ? std::atoi(std::getenv("ACMMP_FUS_AHEAD")) : 6;
         constexpr uint32_t kSpMask = (1u << kSpBits) - 1;
         for (int r = 0; r < H; ++r) {
             const uint32_t *h = vh.hit[(size_t)r].data();
@@ -595,7 +669,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 }
             };
             for (int c = 0; c < W; ++c) {
-                prefetch_to(c + 1 + kAhead);
+                if (kAhead >= 0) prefetch_to(c + 1 + kAhead);
                 const size_t pc = (size_t)r * W + c;
                 const int nh = nhr[c];
                 if (nh == 0xffff) continue;
@@ -668,9 +742,9 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     if (timing)
         std::fprintf(stderr,
                      "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d "
-                     "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu\n",
+                     "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu pinned=%d\n",
                      secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), acmmp_host_threads(), n_live,
-                     n_hits, n_masked, cloud.size());
+                     n_hits, n_masked, cloud.size(), (int)dom.pinned());
     return rc;
 }
 
@@ -737,7 +811,6 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         masks[i].assign((size_t)w * h, 0);
     }
     std::vector<Point> cloud;
-    if (getenv("FUS_RES")) cloud.reserve(6000000);
     Pool pool;
     // Same two-phase scheme as RunFusion: candidates (projection + metrics of
     // both maps) per band of rows on host threads against the current masks,
