@@ -111,7 +111,7 @@ float get_angle(const float *a, const float *b) {  // GetAngle
 // Restored when RunFusion returns. ACMMP_FUSION_PIN=0 turns it off.
 class CacheDomain {
   public:
-    CacheDomain() {
+    CacheDomain() : threads_(acmmp_host_threads()) {  // the budget before any pinning
         if (const char *e = std::getenv("ACMMP_FUSION_PIN"))
             if (std::atoi(e) == 0) return;
         const int cpu = sched_getcpu();
@@ -130,6 +130,7 @@ class CacheDomain {
         if (pinned_) (void)sched_setaffinity(0, sizeof saved_, &saved_);
     }
     bool pinned() const { return pinned_; }
+    int threads() const { return threads_; }
     // worker threads: confine themselves (0 = no limit)
     int workers() const { return pinned_ ? CPU_COUNT(&workers_) : 0; }
     void confine_worker() const {
@@ -164,6 +165,7 @@ class CacheDomain {
         }
         return set;
     }
+    int threads_;
     cpu_set_t saved_{}, workers_{};
     bool pinned_ = false;
 };
@@ -180,7 +182,7 @@ class Pool {
         std::atomic<int> next{0}, done{0};
     };
     explicit Pool(const CacheDomain *dom = nullptr) {
-        int nw = std::max(1, acmmp_host_threads() - 1);
+        int nw = std::max(1, (dom ? dom->threads() : acmmp_host_threads()) - 1);
         if (dom && dom->workers() > 0) nw = std::min(nw, dom->workers());
         for (int t = 0; t < nw; ++t)
             workers_.emplace_back([this, dom] {
@@ -196,6 +198,7 @@ class Pool {
         cv_.notify_all();
         for (auto &t : workers_) t.join();
     }
+    int size() const { return (int)workers_.size(); }
     std::shared_ptr<Job> submit(int n, std::function<void(int)> fn) {
         auto j = std::make_shared<Job>();
         j->fn = std::move(fn);
@@ -651,7 +654,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         auto bit = [](const uint64_t *w, size_t k) -> bool {
             return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
         };
-        static const int kAhead = std::getenv("ACMMP_FUS_AHEAD") ? std::atoi(std::getenv("ACMMP_FUS_AHEAD")) : 6;
+        constexpr int kAhead = 6;  // pixels whose source mask words are prefetched (0, 6, 24: same, r03)
         constexpr uint32_t kSpMask = (1u << kSpBits) - 1;
         for (int r = 0; r < H; ++r) {
             const uint32_t *h = vh.hit[(size_t)r].data();
@@ -669,7 +672,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 }
             };
             for (int c = 0; c < W; ++c) {
-                if (kAhead >= 0) prefetch_to(c + 1 + kAhead);
+                prefetch_to(c + 1 + kAhead);
                 const size_t pc = (size_t)r * W + c;
                 const int nh = nhr[c];
                 if (nh == 0xffff) continue;
@@ -743,7 +746,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::fprintf(stderr,
                      "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d "
                      "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu pinned=%d\n",
-                     secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), acmmp_host_threads(), n_live,
+                     secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), pool.size() + 1, n_live,
                      n_hits, n_masked, cloud.size(), (int)dom.pinned());
     return rc;
 }
