@@ -44,7 +44,8 @@ void usage() {
         "  --view_parallel          multi-GPU: one process per GPU (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/\n"
         "                           MASTER_PORT from the environment, e.g. torchrun --no-python), views\n"
         "                           sharded per pass, depth maps all-gathered (Jacobi order); rank 0 fuses\n"
-        "  --exchange rccl|tcp      view-parallel all-gather: RCCL (default) or TCP via the rendezvous\n"
+        "  --exchange rccl|tcp      view-parallel all-gather: RCCL or TCP via the rendezvous (default:\n"
+        "                           RCCL at world > 1, a device copy at world 1)\n"
         "  --concurrent_views N     view-parallel: engines (HIP streams) per GPU (2)\n");
 }
 
@@ -62,7 +63,7 @@ int main(int argc, char **argv) {
     float consistency_scalar = 0.3f;
     int num_consistent_thresh = 1, single_match_penalty = 0;
     int device = 0, iterations = 0, concurrent_views = 2;
-    bool device_set = false, view_parallel = false, exchange_rccl = true;
+    bool device_set = false, view_parallel = false, exchange_rccl = true, exchange_auto = true;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -93,6 +94,7 @@ int main(int argc, char **argv) {
                 return 2;
             }
             exchange_rccl = e == "rccl";
+            exchange_auto = false;
         } else if (a == "--concurrent_views") {
             concurrent_views = std::atoi(value().c_str());
         } else if (a == "--iterations") {
@@ -190,6 +192,7 @@ int main(int argc, char **argv) {
         vo.geom_iterations = geom_iterations;
         vo.concurrent_views = concurrent_views;
         vo.exchange_rccl = exchange_rccl;
+        vo.exchange_auto = exchange_auto;
         vo.verbose = !quiet;
         const int rc = run_view_parallel(vo);
         if (rc) return rc;

@@ -224,6 +224,7 @@ class Group {
 class Exchange {
   public:
     Exchange(Group &g, bool rccl, int device) : g_(g), rccl_(rccl) {
+        const auto t0 = std::chrono::steady_clock::now();
         hip_check(hipSetDevice(device), "hipSetDevice");
         hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
         if (rccl_) {
@@ -233,6 +234,9 @@ class Exchange {
             const ncclResult_t r = ncclCommInitRank(&comm_, g.world, id, g.rank);
             if (r != ncclSuccess) fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
+        if (std::getenv("ACMMP_HOST_TIMING"))
+            std::fprintf(stderr, "[rank %d] exchange init (%s)=%.2fs\n", g.rank, rccl_ ? "rccl" : "local/tcp",
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     ~Exchange() {
         if (comm_) ncclCommDestroy(comm_);
@@ -817,9 +821,24 @@ int run_view_parallel(const VpOptions &opt) {
         const char *addr = std::getenv("MASTER_ADDR");
         const int port = env_int("ACMMP_RDZV_PORT", env_int("MASTER_PORT", 29500) + 1);
         if (rank < 0 || world < 1 || rank >= world) fail("bad RANK / WORLD_SIZE");
+        if (o.exchange_auto && world == 1) o.exchange_rccl = false;  // nothing to exchange
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         Group g(rank, world, addr && *addr ? addr : "127.0.0.1", port);
-        Driver d(o, g);
-        d.run();
+        double init_s = 0, run_s = 0;
+        clk::time_point t3;
+        {
+            Driver d(o, g);  // problems, LPT, RCCL communicator, engines
+            const auto t1 = clk::now();
+            d.run();
+            const auto t2 = clk::now();
+            init_s = std::chrono::duration<double>(t1 - t0).count();
+            run_s = std::chrono::duration<double>(t2 - t1).count();
+            t3 = clk::now();
+        }
+        if (std::getenv("ACMMP_HOST_TIMING"))
+            std::fprintf(stderr, "[rank %d] init=%.2fs run=%.2fs teardown=%.2fs\n", rank, init_s, run_s,
+                         std::chrono::duration<double>(clk::now() - t3).count());
         if (rank == 0 && o.verbose)
             std::printf("view-parallel: %d ranks (%s exchange), maps under %s%s\n", world,
                         o.exchange_rccl ? "RCCL" : "TCP", o.dense.c_str(), o.output_dir.c_str());

@@ -13,6 +13,8 @@ struct VpOptions {
     int geom_iterations = 2;          // geometric passes per scale (src/main_ACMMP.cpp:109)
     int concurrent_views = 2;         // engines (HIP streams) per GPU
     bool exchange_rccl = true;        // RCCL all-gather, else TCP through the rendezvous
+    bool exchange_auto = true;        // no --exchange: RCCL at world > 1, a device copy at world 1
+                                      // (skips the communicator's ~2.4 s initialisation)
     bool write_outputs = true;        // .dmb maps of every pass
     bool verbose = true;
 };
