@@ -128,14 +128,14 @@ def main():
                          s=res["s"], host_threads=int(nt) if nt else int(_lib().acmmp_host_threads()),
                          cgroup_delta={k: c1[k] - c0.get(k, 0) for k in c1})
         shutil.rmtree(dense + "/ACMMP_dist", ignore_errors=True)
-    if "cli_vp" in STEPS:  # the C++ view-parallel driver, world 1 through RCCL
+    if "cli_vp" in STEPS:  # the C++ view-parallel driver, world 1 (no communicator: a device copy stands for the all-gather)
         cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
         env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT="29611")
         t0 = time.perf_counter()
         subprocess.run([cli, dense, "--view_parallel", "--output_dir", "/ACMMP_cvp", "--no_fusion", "--quiet"],
                        stdout=sys.stderr, check=True, env=env)
-        emit(step="cli_view_parallel_world1", order="jacobi", concurrent_views=2, exchange="rccl",
+        emit(step="cli_view_parallel_world1", order="jacobi", concurrent_views=2, exchange="device copy (world 1 default)",
              s=round(time.perf_counter() - t0, 2))
         shutil.rmtree(dense + "/ACMMP_cvp", ignore_errors=True)
     if "cli" not in STEPS:
