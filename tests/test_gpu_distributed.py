@@ -10,9 +10,11 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from acmmp_amd import io as aio
 from acmmp_amd import scene
 from acmmp_amd.distributed import ViewParallelPipeline
 from oracle_pipeline import OraclePipeline
+from parity_util import assert_bit_exact
 from test_gpu_pipeline import _compare
 
 pytestmark = pytest.mark.gpu
@@ -149,3 +151,27 @@ def test_bench_under_torchrun_nccl_world1():
     res = json.loads(line)
     assert res["n_gpus"] == 1 and res["value"] > 0
     assert "RCCL all-gather" in res["config"]["parallelism"]
+
+
+@pytest.mark.timeout(900)
+def test_world8_split_tail_multi_scale_matches_world1(tmp_path):
+    """The 8-rank path a node runs, rehearsed on the one GPU (8 gloo ranks
+    sharing it): 17 views -> 2 whole views per rank and the 17th split in
+    8 row bands (47 rows each at the coarse scale, 95 at the fine one) in
+    every pass of the multi-scale schedule; every .dmb bit-identical to the
+    world-1 run (which the tests above pin to the oracle)."""
+    d = str(tmp_path / "dense17")
+    sc = scene.make_scene(num_views=17, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=4)
+    got = _spawn(8, d, "gloo", "/VP8")
+    assert all(got[r][1] == [16] for r in range(8))
+    assert sorted(v for r in range(8) for v in got[r][0]) == list(range(17))
+    ViewParallelPipeline(d, "/VP1", device=0).run()
+    n = 0
+    for v in range(17):
+        for name in ("depths", "depths_geom", "normals", "costs"):
+            a = aio.read_dmb(os.path.join(aio.result_folder(d + "/VP8", v), name + ".dmb"))
+            b = aio.read_dmb(os.path.join(aio.result_folder(d + "/VP1", v), name + ".dmb"))
+            assert_bit_exact(a, b, f"view {v} {name}")
+            n += 1
+    assert n == 17 * 4
