@@ -46,7 +46,9 @@ void usage() {
         "                           sharded per pass, depth maps all-gathered (Jacobi order); rank 0 fuses\n"
         "  --exchange rccl|tcp      view-parallel all-gather: RCCL or TCP via the rendezvous (default:\n"
         "                           RCCL at world > 1, a device copy at world 1)\n"
-        "  --concurrent_views N     view-parallel: engines (HIP streams) per GPU (2)\n");
+        "  --concurrent_views N     view-parallel: engines (HIP streams) per GPU (2)\n"
+        "  --no_split_tail          view-parallel: compute the V mod world tail views whole instead of\n"
+        "                           in row bands over all ranks\n");
 }
 
 int die(const char *what) {
@@ -63,7 +65,7 @@ int main(int argc, char **argv) {
     float consistency_scalar = 0.3f;
     int num_consistent_thresh = 1, single_match_penalty = 0;
     int device = 0, iterations = 0, concurrent_views = 2;
-    bool device_set = false, view_parallel = false, exchange_rccl = true, exchange_auto = true;
+    bool device_set = false, view_parallel = false, exchange_rccl = true, exchange_auto = true, split_tail = true;
     unsigned seed = 1234;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -95,6 +97,8 @@ int main(int argc, char **argv) {
             }
             exchange_rccl = e == "rccl";
             exchange_auto = false;
+        } else if (a == "--no_split_tail") {
+            split_tail = false;
         } else if (a == "--concurrent_views") {
             concurrent_views = std::atoi(value().c_str());
         } else if (a == "--iterations") {
@@ -193,6 +197,7 @@ int main(int argc, char **argv) {
         vo.concurrent_views = concurrent_views;
         vo.exchange_rccl = exchange_rccl;
         vo.exchange_auto = exchange_auto;
+        vo.split_tail = split_tail;
         vo.verbose = !quiet;
         const int rc = run_view_parallel(vo);
         if (rc) return rc;

@@ -15,6 +15,11 @@
 //     acmmp_set_plane_hypotheses_device) and exports its results
 //     device-to-device (acmmp_export_results); two engines per GPU, each
 //     on its own HIP stream, take views off a shared queue;
+//   * tail split: the V mod world cheapest views run on ALL ranks as row
+//     bands (acmmp_run_patchmatch_band, 23-row halos all-gathered after
+//     every half-sweep, bands all-gathered afterwards; bit-exact), each with
+//     an owner rank that decodes, gathers and writes it (--no_split_tail
+//     turns it off);
 //   * exchange: the depth maps of a pass go through a padded
 //     [world * slots, Hmax, Wmax] all-gather (ncclAllGather over xGMI, RCCL
 //     has no all-gatherv). Jacobi order: every view of a pass reads the
@@ -366,17 +371,27 @@ class Driver {
         std::sort(order.begin(), order.end(), [&](int a, int b) {
             return cost[(size_t)a] != cost[(size_t)b] ? cost[(size_t)a] > cost[(size_t)b] : a < b;
         });
+        // the tail (V mod world cheapest views) is split over all ranks;
+        // the rest LPT; each split view's owner is the least loaded rank
+        const int ntail = (o.split_tail && g.world > 1) ? n % g.world : 0;
+        split_.assign(order.end() - ntail, order.end());
+        std::sort(split_.begin(), split_.end());
         std::vector<double> load((size_t)g.world, 0.0);
         assignment_.assign((size_t)g.world, {});
-        for (int v : order) {
+        auto place = [&](int v) {
             int r = 0;
             for (int k = 1; k < g.world; ++k)
                 if (load[(size_t)k] < load[(size_t)r]) r = k;
             assignment_[(size_t)r].push_back(v);
             load[(size_t)r] += cost[(size_t)v];
-        }
+        };
+        for (int v : order)
+            if (!is_split(v)) place(v);
+        for (int v : split_) place(v);
         for (auto &a : assignment_) std::sort(a.begin(), a.end());
-        mine_ = assignment_[(size_t)g.rank];
+        owned_ = assignment_[(size_t)g.rank];
+        for (int v : owned_)
+            if (!is_split(v)) mine_.push_back(v);
         for (int k = 0; k < std::max(o.concurrent_views, 1); ++k) {
             acmmp_ctx *ctx = nullptr;
             acmmp_check(acmmp_create(o.device, &ctx), "acmmp_create");
@@ -463,14 +478,14 @@ class Driver {
 
     // a pass's outputs written by 4 host threads while the next pass computes
     void start_writes(bool geom) {
-        const int nw = (int)std::min<size_t>(4, mine_.size());
+        const int nw = (int)std::min<size_t>(4, owned_.size());
         write_errs_.assign((size_t)nw, std::string());
         for (int w = 0; w < nw; ++w)
             writers_.emplace_back([this, w, nw, geom]() {
                 try {
                     hip_check(hipSetDevice(o_.device), "hipSetDevice");
-                    for (size_t k = (size_t)w; k < mine_.size(); k += (size_t)nw)
-                        write_outputs(mine_[k], state_.at(mine_[k]), geom);
+                    for (size_t k = (size_t)w; k < owned_.size(); k += (size_t)nw)
+                        write_outputs(owned_[k], state_.at(owned_[k]), geom);
                 } catch (const std::exception &e) {
                     write_errs_[(size_t)w] = e.what();
                 }
@@ -488,7 +503,9 @@ class Driver {
         images_.clear();
         cams_.clear();
         std::vector<int> need;
-        for (int v : mine_) {
+        std::vector<int> compute_views = mine_;
+        compute_views.insert(compute_views.end(), split_.begin(), split_.end());
+        for (int v : compute_views) {
             const acmmp_problem &p = problems_[(size_t)v];
             need.push_back(p.ref_image_id);
             for (int s = 0; s < p.num_src_images; ++s) need.push_back(p.src_image_ids[s]);
@@ -499,15 +516,15 @@ class Driver {
             if (!index_of_.count(id)) fail("source id " + std::to_string(id) + " is not a problem index");
         // work items: the cameras of every needed image, the pixels of my refs
         std::vector<acmmp_camera> cams(need.size());
-        std::vector<std::vector<float>> host(mine_.size());
-        std::vector<acmmp_camera> own_cams(mine_.size());
-        const size_t nwork = need.size() + mine_.size();
+        std::vector<std::vector<float>> host(owned_.size());
+        std::vector<acmmp_camera> own_cams(owned_.size());
+        const size_t nwork = need.size() + owned_.size();
         std::vector<std::string> errs(nwork);
         std::atomic<size_t> next{0};
         auto worker = [&]() {
             for (size_t k; (k = next++) < nwork;) {
                 const bool pixels = k >= need.size();
-                const int v = pixels ? mine_[k - need.size()] : -1;
+                const int v = pixels ? owned_[k - need.size()] : -1;
                 const int id = pixels ? problems_[(size_t)v].ref_image_id : need[k];
                 acmmp_camera &cam = pixels ? own_cams[k - need.size()] : cams[k];
                 const int size = problems_[(size_t)index_of_.at(id)].cur_image_size;
@@ -529,14 +546,14 @@ class Driver {
         for (auto &t : pool) t.join();
         for (size_t k = 0; k < nwork; ++k)
             if (!errs[k].empty())
-                fail("view " + std::to_string(k < need.size() ? need[k] : problems_[(size_t)mine_[k - need.size()]].ref_image_id) +
+                fail("view " + std::to_string(k < need.size() ? need[k] : problems_[(size_t)owned_[k - need.size()]].ref_image_id) +
                      ": " + errs[k]);
         // my refs: kept contiguous for JBU, and padded into my all-gather slots
         DevBuf send((size_t)slots_ * hmax_ * wmax_);
         hip_check(hipMemset(send.p, 0, send.n * sizeof(float)), "hipMemset");
-        for (size_t k = 0; k < mine_.size(); ++k) {
+        for (size_t k = 0; k < owned_.size(); ++k) {
             const acmmp_camera &c = own_cams[k];
-            const int v = mine_[k];
+            const int v = owned_[k];
             if (c.height != shape_[(size_t)v].first || c.width != shape_[(size_t)v].second)
                 fail("view " + std::to_string(problems_[(size_t)v].ref_image_id) + ": image size disagrees with its header");
             DevBuf d(host[k].size());
@@ -560,6 +577,19 @@ class Driver {
             textures_[need[k]] = t;
             cams_[need[k]] = c;
         }
+        // a split view's JBU runs on every rank: its reference image, unpadded
+        for (int v : split_) {
+            const int id = problems_[(size_t)v].ref_image_id;
+            if (images_.count(id)) continue;
+            const acmmp_camera &c = cams_.at(id);
+            DevBuf d((size_t)c.width * c.height);
+            hip_check(hipMemcpy2DAsync(d.p, (size_t)c.width * sizeof(float), gathered_in(recv_img_, v),
+                                       (size_t)wmax_ * sizeof(float), (size_t)c.width * sizeof(float),
+                                       (size_t)c.height, hipMemcpyDeviceToDevice, copy_[0]),
+                      "hipMemcpy2DAsync");
+            hip_check(hipStreamSynchronize(copy_[0]), "hipStreamSynchronize");
+            images_.emplace(id, std::move(d));
+        }
     }
 
     // (h, w) of every view at this scale (acmmp_load_view's rescale rule)
@@ -579,6 +609,19 @@ class Driver {
             shape_[i] = {h, w};
             hmax = std::max(hmax, h);
             wmax = std::max(wmax, w);
+        }
+        if (!split_checked_) {  // every band must hold the halo at the coarsest scale (this one)
+            split_checked_ = true;
+            std::vector<int> keep;
+            for (int v : split_) {
+                if (shape_[(size_t)v].first >= g_.world * ACMMP_BAND_HALO) {
+                    keep.push_back(v);
+                } else if (std::find(owned_.begin(), owned_.end(), v) != owned_.end()) {
+                    mine_.push_back(v);  // its owner computes it whole
+                    std::sort(mine_.begin(), mine_.end());
+                }
+            }
+            split_ = keep;
         }
         slots_ = 1;
         for (auto &a : assignment_) slots_ = std::max(slots_, (int)a.size());
@@ -618,7 +661,7 @@ class Driver {
     // the gathered depth map of problem i (previous pass)
     const float *gathered(int i) const { return gathered_in(recv_, i); }
 
-    void compute(acmmp_ctx *eng, const Task &t, ViewState &out, hipStream_t cs) {
+    void compute(acmmp_ctx *eng, const Task &t, ViewState &out, hipStream_t cs, bool band = false) {
         const acmmp_problem &pr = problems_[(size_t)t.v];
         std::vector<int> ids = {pr.ref_image_id};
         for (int s = 0; s < pr.num_src_images; ++s) ids.push_back(pr.src_image_ids[s]);
@@ -666,22 +709,151 @@ class Driver {
             acmmp_check(acmmp_set_hierarchy_inputs_device(eng, scaled.p, sw, sh, prev.jbu.p),
                         "acmmp_set_hierarchy_inputs_device", eng);
         }
-        acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
-        if (t.planar) {
-            acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
-            int nsp = 0, ntri = 0;
-            acmmp_check(acmmp_prepare_planar_prior(eng, &nsp, &ntri), "acmmp_prepare_planar_prior", eng);
-            acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
-        }
         out.W = W;
         out.H = H;
         out.planes = DevBuf((size_t)W * H * 4);
         out.costs = DevBuf((size_t)W * H);
         DevBuf depth((size_t)W * H);
-        acmmp_check(acmmp_export_results(eng, out.planes.p, out.costs.p, depth.p), "acmmp_export_results", eng);
-        acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+        if (band) {
+            run_band(eng, t, out, depth, cs);
+        } else {
+            acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
+            if (t.planar) {
+                acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+                int nsp = 0, ntri = 0;
+                acmmp_check(acmmp_prepare_planar_prior(eng, &nsp, &ntri), "acmmp_prepare_planar_prior", eng);
+                acmmp_check(acmmp_run_patchmatch_async(eng), "acmmp_run_patchmatch_async", eng);
+            }
+            acmmp_check(acmmp_export_results(eng, out.planes.p, out.costs.p, depth.p), "acmmp_export_results", eng);
+            acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+        }
         std::lock_guard<std::mutex> lk(mu_);
         depth_tmp_[t.v] = std::move(depth);
+    }
+
+    bool is_split(int v) const { return std::find(split_.begin(), split_.end(), v) != split_.end(); }
+
+    // rows [lo, hi) of band k of H rows over the world (sizes differ by at most 1)
+    std::pair<int, int> band_rows(int H, int k) const {
+        const int base = H / g_.world, extra = H % g_.world;
+        const int lo = k * base + std::min(k, extra);
+        return {lo, lo + base + (k < extra ? 1 : 0)};
+    }
+
+    // The halo exchange of a band run (acmmp_run_patchmatch_band's callback):
+    // each rank all-gathers [rows the band above reads | rows the band below
+    // reads] of the colour just written (plane float4, cost, selected views),
+    // then takes its neighbours' parts. One all-gather of 2 x 23 rows per
+    // rank and half-sweep (RCCL over xGMI, or the TCP exchange).
+    struct BandCtx {
+        Driver *d;
+        hipStream_t cs;
+        DevBuf send, recv;
+        std::string err;
+    };
+    static int band_exchange(void *user, const acmmp_band_halo *h) {
+        BandCtx *b = static_cast<BandCtx *>(user);
+        try {
+            b->d->halo_exchange(*b, *h);
+            return 0;
+        } catch (const std::exception &e) {
+            b->err = e.what();
+            return 1;
+        }
+    }
+    void halo_exchange(BandCtx &b, const acmmp_band_halo &h) {
+        const size_t Wh = (size_t)h.Wh, K = ACMMP_BAND_HALO;
+        const size_t part = K * Wh * 6;  // floats: K rows of plane (4) + cost + selected views
+        if (b.send.n != 2 * part) {
+            b.send = DevBuf(2 * part);
+            b.recv = DevBuf(2 * part * (size_t)g_.world);
+        }
+        // the sweep that wrote these rows ran on the engine's stream
+        hip_check(hipStreamSynchronize((hipStream_t)h.stream), "hipStreamSynchronize");
+        auto pack = [&](float *dst, int lo, int hi) {
+            const size_t n = (size_t)(hi - lo) * Wh;
+            if (!n) return;
+            hip_check(hipMemcpyAsync(dst, (const float *)h.plane + (size_t)lo * Wh * 4, n * 16, hipMemcpyDeviceToDevice,
+                                     b.cs), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(dst + K * Wh * 4, (const float *)h.cost + (size_t)lo * Wh, n * 4,
+                                     hipMemcpyDeviceToDevice, b.cs), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(dst + K * Wh * 5, (const uint32_t *)h.sv + (size_t)lo * Wh, n * 4,
+                                     hipMemcpyDeviceToDevice, b.cs), "hipMemcpyAsync");
+        };
+        auto unpack = [&](const float *src, int lo, int hi) {
+            const size_t n = (size_t)(hi - lo) * Wh;
+            if (!n) return;
+            hip_check(hipMemcpyAsync((float *)h.plane + (size_t)lo * Wh * 4, src, n * 16, hipMemcpyDeviceToDevice, b.cs),
+                      "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync((float *)h.cost + (size_t)lo * Wh, src + K * Wh * 4, n * 4,
+                                     hipMemcpyDeviceToDevice, b.cs), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync((uint32_t *)h.sv + (size_t)lo * Wh, src + K * Wh * 5, n * 4,
+                                     hipMemcpyDeviceToDevice, b.cs), "hipMemcpyAsync");
+        };
+        pack(b.send.p, h.send_up_lo, h.send_up_hi);
+        pack(b.send.p + part, h.send_down_lo, h.send_down_hi);
+        hip_check(hipStreamSynchronize(b.cs), "hipStreamSynchronize");
+        ex_.allgather(b.send.p, b.recv.p, b.send.n);
+        const int r = g_.rank;
+        if (r > 0) unpack(b.recv.p + (size_t)(r - 1) * 2 * part + part, h.recv_up_lo, h.recv_up_hi);
+        if (r + 1 < g_.world) unpack(b.recv.p + (size_t)(r + 1) * 2 * part, h.recv_down_lo, h.recv_down_hi);
+        // the engine's next sweep is enqueued after this returns
+        hip_check(hipStreamSynchronize(b.cs), "hipStreamSynchronize");
+    }
+
+    // every band's rows of the exported (planes, costs) from its rank, on every rank
+    void gather_bands(ViewState &out, hipStream_t cs) {
+        const int W = out.W, H = out.H;
+        int rmax = 0;
+        for (int k = 0; k < g_.world; ++k) rmax = std::max(rmax, band_rows(H, k).second - band_rows(H, k).first);
+        const size_t per = (size_t)rmax * W * 5;
+        DevBuf send(per), recv(per * (size_t)g_.world);
+        const auto [lo, hi] = band_rows(H, g_.rank);
+        hip_check(hipMemcpyAsync(send.p, out.planes.p + (size_t)lo * W * 4, (size_t)(hi - lo) * W * 16,
+                                 hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync");
+        hip_check(hipMemcpyAsync(send.p + (size_t)rmax * W * 4, out.costs.p + (size_t)lo * W, (size_t)(hi - lo) * W * 4,
+                                 hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
+        ex_.allgather(send.p, recv.p, per);
+        for (int k = 0; k < g_.world; ++k) {
+            if (k == g_.rank) continue;
+            const auto [blo, bhi] = band_rows(H, k);
+            const float *src = recv.p + (size_t)k * per;
+            hip_check(hipMemcpyAsync(out.planes.p + (size_t)blo * W * 4, src, (size_t)(bhi - blo) * W * 16,
+                                     hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(out.costs.p + (size_t)blo * W, src + (size_t)rmax * W * 4,
+                                     (size_t)(bhi - blo) * W * 4, hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync");
+        }
+        hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
+    }
+
+    // One view's run split in row bands over every rank (the engine already
+    // holds the view's inputs): this rank's band, the halos exchanged every
+    // half-sweep, the bands gathered; with the planar prior, the prior is
+    // rebuilt on every rank from the gathered first run, then the second run
+    // (src/acmmp_definitions.cpp:306-379). `depth` = the planes' w channel.
+    void run_band(acmmp_ctx *eng, const Task &t, ViewState &out, DevBuf &depth, hipStream_t cs) {
+        const auto [lo, hi] = band_rows(out.H, g_.rank);
+        BandCtx b{this, cs, {}, {}, {}};
+        for (int run = 0; run < (t.planar ? 2 : 1); ++run) {
+            if (run) {
+                acmmp_check(acmmp_set_plane_hypotheses_device(eng, out.planes.p, out.costs.p),
+                            "acmmp_set_plane_hypotheses_device", eng);
+                int nsp = 0, ntri = 0;
+                acmmp_check(acmmp_prepare_planar_prior(eng, &nsp, &ntri), "acmmp_prepare_planar_prior", eng);
+            }
+            const int rc = acmmp_run_patchmatch_band(eng, lo, hi, &Driver::band_exchange, &b);
+            if (!b.err.empty()) fail("band exchange: " + b.err);
+            acmmp_check(rc, "acmmp_run_patchmatch_band", eng);
+            acmmp_check(acmmp_export_results(eng, out.planes.p, out.costs.p, nullptr), "acmmp_export_results", eng);
+            acmmp_check(acmmp_synchronize(eng), "acmmp_synchronize", eng);
+            gather_bands(out, cs);
+        }
+        const size_t P = (size_t)out.W * out.H;
+        hip_check(hipMemcpy2DAsync(depth.p, sizeof(float), out.planes.p + 3, 4 * sizeof(float), sizeof(float), P,
+                                   hipMemcpyDeviceToDevice, cs),
+                  "hipMemcpy2DAsync");
+        hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
     }
 
     void write_outputs(int v, const ViewState &s, bool geom) {
@@ -712,6 +884,10 @@ class Driver {
             next[v];
             state_[v];
         }
+        for (int v : split_) {
+            next[v];
+            state_[v];
+        }
         // views off a shared queue, one host thread per engine
         std::atomic<size_t> q{0};
         std::vector<std::string> errs(engines_.size());
@@ -732,6 +908,10 @@ class Driver {
         }
         for (auto &e : errs)
             if (!e.empty()) fail(e);
+        if (!split_.empty()) {  // the tail views, every rank on a band of each
+            Clock c(this, "split_compute");
+            for (int v : split_) compute(engines_[0], Task{v, geom, planar, hier, multi}, next[v], copy_[0], true);
+        }
         {
             Clock c(this, "flush_writes");
             flush_writes();  // the previous pass's writers still read the state replaced below
@@ -740,8 +920,10 @@ class Driver {
         // state, then the padded all-gather of the depth maps; the outputs are
         // written while the next pass computes
         hip_check(hipMemset(send_.p, 0, send_.n * sizeof(float)), "hipMemset");
-        for (size_t k = 0; k < mine_.size(); ++k) {
-            const int v = mine_[k];
+        for (int v : split_)  // every rank holds the split views' full state
+            if (std::find(owned_.begin(), owned_.end(), v) == owned_.end()) state_[v] = std::move(next[v]);
+        for (size_t k = 0; k < owned_.size(); ++k) {
+            const int v = owned_[k];
             ViewState &s = next[v];
             hip_check(hipMemcpy2D(send_.p + k * (size_t)hmax_ * wmax_, (size_t)wmax_ * sizeof(float),
                                   depth_tmp_.at(v).p, (size_t)s.W * sizeof(float), (size_t)s.W * sizeof(float),
@@ -760,7 +942,9 @@ class Driver {
     // this scale's image (src/ACMMP.cpp:964-1087) on the device, kept there
     // for the hierarchy pass
     void jbu() {
-        for (int v : mine_) {
+        std::vector<int> views = mine_;
+        views.insert(views.end(), split_.begin(), split_.end());
+        for (int v : views) {
             ViewState &s = state_[v];
             const int id = problems_[(size_t)v].ref_image_id;
             const acmmp_camera &c = cams_.at(id);
@@ -787,7 +971,10 @@ class Driver {
     std::map<int, int> index_of_;
     int max_down_ = -1;
     std::vector<std::vector<int>> assignment_;
-    std::vector<int> mine_;
+    std::vector<int> mine_;   // views this rank computes whole
+    std::vector<int> owned_;  // views whose image / depth slot and .dmb files are this rank's
+    std::vector<int> split_;  // views every rank computes a band of
+    bool split_checked_ = false;
     std::vector<acmmp_ctx *> engines_;
     std::vector<hipStream_t> copy_;  // per engine: the driver's device-to-device copies
     std::map<int, DevBuf> images_;

@@ -15,6 +15,7 @@ struct VpOptions {
     bool exchange_rccl = true;        // RCCL all-gather, else TCP through the rendezvous
     bool exchange_auto = true;        // no --exchange: RCCL at world > 1, a device copy at world 1
                                       // (skips the communicator's ~2.4 s initialisation)
+    bool split_tail = true;           // the V mod world cheapest views in row bands over all ranks
     bool write_outputs = true;        // .dmb maps of every pass
     bool verbose = true;
 };

@@ -66,11 +66,15 @@ def test_world1_rccl_matches_oracle_jacobi(dense, jacobi_maps):
     assert _compare(dense + "/CVP1", jacobi_maps) == 5 * 4
 
 
-def test_world2_tcp_matches_oracle_jacobi_and_fuses(dense, jacobi_maps):
-    _launch(dense, "/CVP2", 2, "tcp")
-    assert _compare(dense + "/CVP2", jacobi_maps) == 5 * 4
+@pytest.mark.parametrize("split", [True, False])
+def test_world2_tcp_matches_oracle_jacobi_and_fuses(dense, jacobi_maps, split):
+    """5 views on 2 ranks: by default the 5th is computed by both ranks as
+    two row bands (halos all-gathered after every half-sweep)."""
+    out = "/CVP2" if split else "/CVP2w"
+    _launch(dense, out, 2, "tcp", [] if split else ["--no_split_tail"])
+    assert _compare(dense + out, jacobi_maps) == 5 * 4
     # rank 0 fused the maps after the last pass (main_ACMMP's RunFusion)
-    assert os.path.getsize(os.path.join(dense + "/CVP2", "ACMMP_model.ply")) > 1000
+    assert os.path.getsize(os.path.join(dense + out, "ACMMP_model.ply")) > 1000
 
 
 @pytest.mark.timeout(900)
@@ -83,6 +87,19 @@ def test_world2_tcp_multi_scale_matches_oracle_jacobi(tmp_path):
     _launch(d, "/CVPMS", 2, "tcp", ["--no_fusion"], timeout=600)
     maps = OraclePipeline(d).run_multi_scale("jacobi")
     assert _compare(d + "/CVPMS", maps) == 4 * 4
+
+
+@pytest.mark.timeout(900)
+def test_world2_tcp_multi_scale_split_tail_matches_oracle_jacobi(tmp_path):
+    """3 views on 2 ranks through the multi-scale schedule: the third view in
+    two row bands in every pass (planar prior rebuilt on both ranks, JBU and
+    hierarchy inputs on both), every .dmb bit-exact."""
+    d = str(tmp_path / "dense_ms3")
+    sc = scene.make_scene(num_views=3, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=2)
+    _launch(d, "/CVPMS3", 2, "tcp", ["--no_fusion"], timeout=600)
+    maps = OraclePipeline(d).run_multi_scale("jacobi")
+    assert _compare(d + "/CVPMS3", maps) == 3 * 4
 
 
 @pytest.mark.timeout(900)
