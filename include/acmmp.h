@@ -349,15 +349,15 @@ int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
 
 /* Hardware self-test: compares v_rcp_f32 + one Newton step with the IEEE
  * division 1/z for every float32 in the fast-reciprocal exponent window
- * (2^-125 <= |z| < 2^125). mismatches == 0 proves the ACMMP_FAST_RCP build
+ * (2^-125 <= |z| < 2^125). mismatches == 0 proves the sweep's fast reciprocal
  * bit-identical to the pinned division on this device. */
 int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked);
 
 /* Texel storage the gather kernels use for the current images (set by
- * acmmp_set_images*): 16 = f16 difference quads (the default whenever every
- * stored value is exact in f16, e.g. 8-bit JPEG input), 8 = u8 quads (on
- * request, ACMMP_TEXEL=u8, every view integer-valued in [0, 255]), 32 = fp32
- * row pairs (any other input, or ACMMP_TEXEL=f32). Results are identical in
+ * acmmp_set_images*): 8 = u8 quads (the default whenever every view is
+ * integer-valued in [0, 255], e.g. 8-bit JPEG input), 16 = f16 difference
+ * quads (every stored value exact in f16, or ACMMP_TEXEL=h16), 32 = fp32 row
+ * pairs (any other input, or ACMMP_TEXEL=f32). Results are identical in
  * every form; this reports the memory format only. No reference counterpart
  * (diagnostic). */
 int acmmp_get_texel_bits(const acmmp_ctx *ctx);
