@@ -634,6 +634,12 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         return pool.submit(rows[i], [&, i](int r) { phase1(i, vhits[i & 1], r); });
     };
     std::vector<Point> cloud;
+    {  // at most one point per pixel: reserve the address range once (pages
+       // are committed as points arrive), no reallocation copies in the walk
+        size_t cap = 0;
+        for (size_t i = 0; i < n; ++i) cap += (size_t)cols[i] * rows[i];
+        cloud.reserve(cap);
+    }
     const auto t_loaded = now();
     auto job = start_phase1(0);
     for (size_t i = 0; i < n; ++i) {
@@ -814,6 +820,11 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         masks[i].assign((size_t)w * h, 0);
     }
     std::vector<Point> cloud;
+    {  // at most one point per pixel (see RunFusion)
+        size_t cap = 0;
+        for (size_t i = 0; i < n; ++i) cap += (size_t)in.cols[i] * in.rows[i];
+        cloud.reserve(cap);
+    }
     Pool pool;
     // Same two-phase scheme as RunFusion: candidates (projection + metrics of
     // both maps) per band of rows on host threads against the current masks,
