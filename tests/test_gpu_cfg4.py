@@ -144,3 +144,22 @@ def test_full_cfg4_drivers_agree_and_match_geometry(full_cfg4):
     print("view, confident share, median rel. error, share within 1 %:", errs)
     assert min(e[1] for e in errs) > 0.1, f"too few confident pixels: {errs}"
     assert max(e[2] for e in errs) < 0.01, f"median relative depth error per view: {errs}"
+
+
+@pytest.mark.timeout(1200)
+def test_full_cfg4_cpp_driver_world8_matches_world1(full_cfg4):
+    """cfg4's full shape at BASELINE's 8 ranks: 8 acmmp_main ranks sharing the
+    box's one GPU (TCP exchange; RCCL refuses several ranks on one device),
+    6 whole views per rank and the 49th view of every pass split in 8 row
+    bands. Every .dmb must equal the world-1 run's byte for byte."""
+    d, _ = full_cfg4
+    if not os.path.isdir(d + "/F4CPP"):  # the world-1 maps of the test above
+        _launch(d, "/F4CPP", 1, "rccl", ["--no_fusion"], timeout=1000)
+    _launch(d, "/F4CPP8", 8, "tcp", ["--no_fusion"], timeout=1000)
+    names = ("depths", "depths_geom", "normals", "costs")
+    for v in range(FULL_VIEWS):
+        for name in names:
+            a = os.path.join(aio.result_folder(d + "/F4CPP", v), name + ".dmb")
+            b = os.path.join(aio.result_folder(d + "/F4CPP8", v), name + ".dmb")
+            with open(a, "rb") as fa, open(b, "rb") as fb:
+                assert fa.read() == fb.read(), f"view {v} {name}: world 8 differs from world 1"
