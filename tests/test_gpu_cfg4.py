@@ -163,3 +163,25 @@ def test_full_cfg4_cpp_driver_world8_matches_world1(full_cfg4):
             b = os.path.join(aio.result_folder(d + "/F4CPP8", v), name + ".dmb")
             with open(a, "rb") as fa, open(b, "rb") as fb:
                 assert fa.read() == fb.read(), f"view {v} {name}: world 8 differs from world 1"
+
+
+@pytest.mark.timeout(1200)
+def test_full_cfg4_python_driver_world8_matches_world1(full_cfg4):
+    """The same at world 8 through acmmp_amd.distributed (8 gloo ranks
+    sharing the one GPU): every .dmb byte-identical to the world-1 run."""
+    from acmmp_amd.distributed import ViewParallelPipeline
+    from test_gpu_distributed import _spawn
+    d, _ = full_cfg4
+    if not os.path.isdir(d + "/F4PY"):
+        ViewParallelPipeline(d, "/F4PY", device=0).run()
+    got = _spawn(8, d, "gloo", "/F4PY8")
+    splits = {tuple(got[r][1]) for r in range(8)}
+    assert len(splits) == 1 and len(next(iter(splits))) == FULL_VIEWS % 8, got  # the tail view, in 8 bands
+    assert sorted(v for r in range(8) for v in got[r][0]) == list(range(FULL_VIEWS))
+    names = ("depths", "depths_geom", "normals", "costs")
+    for v in range(FULL_VIEWS):
+        for name in names:
+            a = os.path.join(aio.result_folder(d + "/F4PY", v), name + ".dmb")
+            b = os.path.join(aio.result_folder(d + "/F4PY8", v), name + ".dmb")
+            with open(a, "rb") as fa, open(b, "rb") as fb:
+                assert fa.read() == fb.read(), f"view {v} {name}: world 8 differs from world 1"
