@@ -174,6 +174,7 @@ SIGNATURES = {
     "acmmp_set_images_device": (C.c_int, [_CTX, C.c_int, C.POINTER(Camera), C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_int32), C.c_int]),
     "acmmp_set_plane_hypotheses_device": (C.c_int, [_CTX, C.c_void_p, C.c_void_p]),
+    "acmmp_wait_stream": (C.c_int, [_CTX, C.c_void_p]),
     "acmmp_texture_create": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "acmmp_texture_destroy": (None, [C.c_void_p]),
     "acmmp_texture_bits": (C.c_int, [C.c_void_p]),

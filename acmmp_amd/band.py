@@ -108,21 +108,25 @@ class TorchBandExchange:
 def gather_bands(planes: torch.Tensor, costs: torch.Tensor, bands_: list, members: list, index: int,
                  comm_device: torch.device, group=None):
     """Every band's rows of (H, W, 4) planes and (H, W) costs from its rank,
-    assembled in place on every participant."""
+    assembled in place on every participant. The assembly is enqueued on
+    torch's current stream (through gloo: pinned staging buffers and
+    asynchronous host-to-device copies); an engine reading the result orders
+    its stream after torch's first (ACMMP._after_producer)."""
+    if len(members) == 1:
+        return planes, costs
     H, W = costs.shape
     rmax = max(hi - lo for lo, hi in bands_)
     lo, hi = bands_[index]
     send = torch.zeros((rmax, W, 5), dtype=torch.float32, device=comm_device)
     send[:hi - lo, :, :4] = planes[lo:hi].to(comm_device)
     send[:hi - lo, :, 4] = costs[lo:hi].to(comm_device)
-    if len(members) == 1:
-        return planes, costs
-    recv = [torch.empty_like(send) for _ in members]
+    pin = comm_device.type == "cpu" and planes.is_cuda
+    recv = [torch.empty(send.shape, dtype=send.dtype, device=comm_device, pin_memory=pin) for _ in members]
     dist.all_gather(recv, send, group=group)
     for k, (blo, bhi) in enumerate(bands_):
         if k == index:
             continue
-        r = recv[k].to(planes.device)
+        r = recv[k].to(planes.device, non_blocking=True)
         planes[blo:bhi] = r[:bhi - blo, :, :4]
         costs[blo:bhi] = r[:bhi - blo, :, 4]
     return planes, costs
@@ -145,7 +149,8 @@ def run_split(eng, bands_: list, members: list, index: int, device: torch.device
         gather_bands(planes, costs, bands_, members, index, comm_device, group)
         if planar_prior and run == 0:
             # support points + Delaunay need the whole image: every rank
-            # builds the same prior from the gathered state
+            # builds the same prior from the gathered state (the engine's
+            # copy waits for the assembly on torch's stream)
             eng.set_plane_hypotheses_device(planes.data_ptr(), costs.data_ptr())
             eng.prepare_planar_prior()
     return planes, costs

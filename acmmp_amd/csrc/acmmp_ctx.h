@@ -87,6 +87,9 @@ struct acmmp_ctx {
     acmmp_timing last_timing{};
     hipEvent_t ev[8] = {};
     bool events_made = false;
+
+    // acmmp_wait_stream: recorded on a producer stream, waited on by `stream`
+    hipEvent_t wait_ev = nullptr;
 };
 
 namespace acmmp {

@@ -461,6 +461,7 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     }
     if (ctx->events_made)
         for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+    if (ctx->wait_ev) (void)hipEventDestroy(ctx->wait_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -637,6 +638,17 @@ int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, co
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, d_planes4, P * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_cost, d_costs, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     ctx->have_state = true;
+    return ACMMP_OK;
+}
+
+int acmmp_wait_stream(acmmp_ctx *ctx, void *stream) {
+    if (!ctx) return ACMMP_ERR_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->wait_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->wait_ev, hipEventDisableTiming));
+    // hipStreamWaitEvent captures the event's state at this call, so the one
+    // event is safely re-recorded by the next call
+    HIP_TRY(ctx, hipEventRecord(ctx->wait_ev, (hipStream_t)stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->wait_ev, 0));
     return ACMMP_OK;
 }
 

@@ -9,6 +9,7 @@ native HIP engine — there is no CPU fallback: a missing library or GPU raises.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from typing import Sequence
 
 import numpy as np
@@ -148,6 +149,7 @@ class ACMMP:
             raise AcmmpError(f"acmmp_create(device={device}) failed with status {rc} "
                              "(no HIP device visible?)")
         self._ctx = ctx
+        self.device = int(device)
         self._keep = []  # host buffers referenced by the last upload
         if params is not None:
             self.set_params(params)
@@ -229,9 +231,28 @@ class ACMMP:
         ptrs = (C.POINTER(C.c_float) * len(ds))(*[_fptr(d) for d in ds])
         self._check(self._lib.acmmp_set_depth_maps(self._ctx, ptrs), "acmmp_set_depth_maps")
 
+    def wait_stream(self, stream_handle: int | None):
+        """acmmp_wait_stream: the engine stream waits (on the device, no host
+        wait) for everything enqueued so far on `stream_handle` (a
+        hipStream_t; 0/None = the legacy default stream)."""
+        self._check(self._lib.acmmp_wait_stream(self._ctx, C.c_void_p(int(stream_handle or 0) or None)),
+                    "acmmp_wait_stream")
+
+    def _after_producer(self):
+        """Orders the engine stream (non-blocking) after torch's current stream
+        on this device before a *_device setter borrows or copies a caller
+        buffer: buffers the caller built with torch ops (a gathered band, a
+        collective's output, a torch.cat) may still be being written there.
+        A no-op when torch is not loaded or has not touched the GPU."""
+        torch = sys.modules.get("torch")
+        if torch is None or not torch.cuda.is_initialized():
+            return
+        self.wait_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
     def set_depth_maps_device(self, device_ptrs: Sequence[int], pitches: Sequence[int] | None = None):
         """Borrow device-resident depth maps (e.g. slices of an RCCL
         all-gather); the caller keeps them alive until the run completes."""
+        self._after_producer()
         arr = (C.c_void_p * len(device_ptrs))(*[C.c_void_p(int(p)) for p in device_ptrs])
         pit = None if pitches is None else (C.c_int32 * len(pitches))(*pitches)
         self._check(self._lib.acmmp_set_depth_maps_device(self._ctx, arr, pit), "acmmp_set_depth_maps_device")
@@ -239,6 +260,7 @@ class ACMMP:
     def set_images_device(self, cams: Sequence[_abi.Camera], device_ptrs: Sequence[int],
                           pitches: Sequence[int] | None = None, keep_depth_range: bool = False):
         """Zero-copy set_images: borrow device-resident images."""
+        self._after_producer()
         n = len(cams)
         cam_arr = (_abi.Camera * n)(*cams)
         arr = (C.c_void_p * n)(*[C.c_void_p(int(p)) for p in device_ptrs])
@@ -249,6 +271,7 @@ class ACMMP:
     def set_images_textures(self, cams: Sequence[_abi.Camera], textures: Sequence["Texture"],
                             keep_depth_range: bool = False):
         """set_images_device from prebuilt textures (no per-run padding)."""
+        self._after_producer()
         n = len(cams)
         cam_arr = (_abi.Camera * n)(*cams)
         arr = (C.c_void_p * n)(*[t.handle for t in textures])
@@ -256,13 +279,20 @@ class ACMMP:
                     "acmmp_set_images_textures")
 
     def set_plane_hypotheses_device(self, d_planes: int, d_costs: int):
+        """Previous state from device buffers, copied on the engine stream
+        after the producer's writes (acmmp_wait_stream)."""
+        self._after_producer()
         self._check(self._lib.acmmp_set_plane_hypotheses_device(self._ctx, C.c_void_p(int(d_planes)),
                                                                 C.c_void_p(int(d_costs))),
                     "acmmp_set_plane_hypotheses_device")
 
     def export_results(self, d_planes: int = 0, d_costs: int = 0, d_depth: int = 0):
         """Device-to-device copy of the last results (enqueued on the engine
-        stream; call synchronize() before another stream reads them)."""
+        stream; call synchronize() before another stream reads them). The
+        copy is ordered after torch's current stream: the destination may be
+        memory torch's allocator just recycled from a tensor still in use
+        there."""
+        self._after_producer()
         self._check(self._lib.acmmp_export_results(self._ctx, C.c_void_p(int(d_planes) or None),
                                                    C.c_void_p(int(d_costs) or None),
                                                    C.c_void_p(int(d_depth) or None)),
@@ -287,6 +317,7 @@ class ACMMP:
         """Hierarchy inputs from device buffers (scaled planes scaled_h x
         scaled_w float4, upsampled depth at the reference size); they must
         stay valid until the next run has completed."""
+        self._after_producer()
         self._check(self._lib.acmmp_set_hierarchy_inputs_device(self._ctx, C.c_void_p(int(d_scaled_planes)),
                                                                 int(scaled_w), int(scaled_h),
                                                                 C.c_void_p(int(d_upsampled_depth))),

@@ -195,8 +195,21 @@ int acmmp_set_images_textures(acmmp_ctx *ctx, int num_images, const acmmp_camera
 /* Previous-pass state for the reuse init branch (src/ACMMP.cpp:718-742):
  * planes = (world-frame normal xyz, depth) float4 per ref pixel, costs per pixel. */
 int acmmp_set_plane_hypotheses(acmmp_ctx *ctx, const float *planes4, const float *costs);
-/* Same from device buffers (copied device-to-device on the engine stream). */
+/* Same from device buffers (copied device-to-device on the engine stream).
+ * The engine stream does NOT wait for other streams: work that produced the
+ * buffers on another stream must be complete, or ordered first with
+ * acmmp_wait_stream. */
 int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, const float *d_costs);
+
+/* Orders the engine stream after everything enqueued so far on `stream` (a
+ * hipStream_t of the same device; NULL = the legacy default stream): an event
+ * recorded on `stream` that the engine stream waits on, no host wait. Every
+ * *_device setter borrows or copies caller buffers on the engine stream,
+ * which is created non-blocking; a producer on another stream (a torch
+ * collective, a torch copy) must be ordered with this call first. The
+ * reference has one blocking default stream and needs no such call
+ * (src/ACMMP.cpp:638-831). */
+int acmmp_wait_stream(acmmp_ctx *ctx, void *stream);
 
 /* Hierarchy inputs (src/ACMMP.cpp:745-808): low-res scaled planes
  * (normal xyz + cost-or-depth in w) of size scaled_h*scaled_w, and the

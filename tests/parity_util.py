@@ -30,3 +30,35 @@ def rel_depth_agreement(gpu_planes, ref_planes, costs, tol=1e-3):
     n_err = np.abs(gpu_planes[..., :3] - ref_planes[..., :3]).max(axis=-1)
     ok = (rel <= tol) & (n_err <= tol)
     return float(ok[m].mean()) if m.any() else 1.0
+
+
+def dmb_tree_diffs(folder_a, folder_b, views, names=("depths", "depths_geom", "normals", "costs")):
+    """Every (view, map) whose .dmb differs byte-wise between two output
+    trees, with the number of differing elements and the first one's
+    (row, col): all of them, so a failure shows which view and pass
+    diverged first instead of stopping at the first file."""
+    import os
+    from acmmp_amd import io as aio
+    out = []
+    for v in views:
+        for name in names:
+            pa = os.path.join(aio.result_folder(folder_a, v), name + ".dmb")
+            pb = os.path.join(aio.result_folder(folder_b, v), name + ".dmb")
+            with open(pa, "rb") as fa, open(pb, "rb") as fb:
+                if fa.read() == fb.read():
+                    continue
+            a, b = aio.read_dmb(pa), aio.read_dmb(pb)
+            if a.shape != b.shape:
+                out.append((v, name, f"shape {a.shape} vs {b.shape}"))
+                continue
+            bad = mismatch(a, b)
+            first = np.argwhere(bad)[0].tolist() if bad.any() else None
+            out.append((v, name, f"{int(bad.sum())} elements differ, first at {first}"))
+    return out
+
+
+def assert_dmb_trees_equal(folder_a, folder_b, views, what, names=("depths", "depths_geom", "normals", "costs")):
+    diffs = dmb_tree_diffs(folder_a, folder_b, views, names)
+    if diffs:
+        lines = "\n".join(f"  view {v} {n}: {d}" for v, n, d in diffs)
+        raise AssertionError(f"{what}: {len(diffs)} of {len(views) * len(names)} maps differ:\n{lines}")

@@ -62,7 +62,24 @@ def _setup(eng, mode, W, H):
         eng.SetPlanarPrior(truth)
 
 
-def _worker(rank, world, port, mode, W, H, q):
+def _delay_band_gather(cycles):
+    """Queues a GPU spin on torch's stream right after the bands' all-gather
+    returns, so the torch copies that assemble the gathered bands into the
+    planes/costs tensors (band.gather_bands) land ~`cycles` GPU clocks late:
+    an engine-stream consumer that is not ordered after torch's stream (the
+    r03 race: set_plane_hypotheses_device before the planar prior is built)
+    then reads a partly assembled buffer in every run, not by chance."""
+    import acmmp_amd.band as band
+    orig = band.dist.all_gather
+
+    def slow(*a, **k):
+        r = orig(*a, **k)
+        torch.cuda._sleep(int(cycles))
+        return r
+    band.dist.all_gather = slow
+
+
+def _worker(rank, world, port, mode, W, H, q, delay=0):
     import datetime
     import traceback
     # a failing rank must not leave the others waiting for its halos
@@ -70,6 +87,12 @@ def _worker(rank, world, port, mode, W, H, q):
                             timeout=datetime.timedelta(seconds=60))
     try:
         from acmmp_amd.band import bands, run_split
+        if delay:
+            _delay_band_gather(delay)
+            if os.environ.get("ACMMP_TEST_UNORDERED") == "1":
+                # negative control (run by hand): the engine no longer waits
+                # on torch's stream, and this test must then fail
+                ACMMP._after_producer = lambda self: None
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         with ACMMP(0) as eng:
@@ -96,13 +119,11 @@ def _unsplit(mode, W, H):
         return eng.plane_hypotheses(), eng.costs()
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 120, 100), (3, 96, 77)])
-@pytest.mark.parametrize("mode", MODES)
-def test_band_split_matches_unsplit(mode, world, W, H):
+def _run_bands(mode, world, W, H, delay=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, W, H, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, W, H, q, delay)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=150)
@@ -113,3 +134,104 @@ def test_band_split_matches_unsplit(mode, world, W, H):
     ref = _unsplit(mode, W, H)
     assert_bit_exact(got[1], ref[0], f"{mode}: planes, {world} bands")
     assert_bit_exact(got[2], ref[1], f"{mode}: costs, {world} bands")
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 120, 100), (3, 96, 77)])
+@pytest.mark.parametrize("mode", MODES)
+def test_band_split_matches_unsplit(mode, world, W, H):
+    _run_bands(mode, world, W, H)
+
+
+def test_band_split_planar_with_late_torch_stream():
+    """Regression for GPUTEST_r03's world-8 mismatch: the planar-prior
+    second run starts from the gathered bands, which torch assembles on its
+    own stream; here that stream is held ~0.2 s behind (torch.cuda._sleep)
+    so an engine-side copy that does not wait for it reads stale rows in
+    every run. With the ordering (ACMMP._after_producer ->
+    acmmp_wait_stream) the split stays bit-identical to the unsplit run."""
+    _run_bands("planar", 2, 160, 120, delay=400_000_000)
+
+
+# --------------------------------------------------------------- cfg5
+CFG5_W, CFG5_H, CFG5_SRC, CFG5_ITERS = 6048, 4032, 9, 8
+
+
+def _cfg5_inputs():
+    """cfg5 (BASELINE configs[4]): one ETH3D-size view with 9 sources,
+    rendered straight into HBM (the same bytes in every process)."""
+    setup = scene.scene_setup(num_views=CFG5_SRC + 1, width=CFG5_W, height=CFG5_H)
+    ids = [0] + list(setup.pairs[0][:CFG5_SRC])
+    dev = torch.device("cuda", 0)
+    imgs = [scene.render_torch(setup, i, dev) for i in ids]
+    torch.cuda.synchronize()
+    cams = [setup.camera(i) for i in ids]
+    p = default_params()
+    p.max_iterations = CFG5_ITERS
+    return cams, imgs, p
+
+
+def _cfg5_worker(rank, world, port, out, q):
+    import datetime
+    import time
+    import traceback
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=120))
+    try:
+        from acmmp_amd.band import bands, run_split
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        cams, imgs, p = _cfg5_inputs()
+        with ACMMP(0) as eng:
+            eng.set_params(p)
+            eng.set_images_device(cams, [im.data_ptr() for im in imgs])
+            dist.barrier()
+            t0 = time.perf_counter()
+            planes, costs = run_split(eng, bands(CFG5_H, world), list(range(world)), rank, dev,
+                                      torch.device("cpu"))
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if rank == 0:
+                np.save(out + "_planes.npy", planes.cpu().numpy())
+                np.save(out + "_costs.npy", costs.cpu().numpy())
+        q.put(("ok", rank, dt))
+    except BaseException:
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_cfg5_two_bands_matches_unsplit(tmp_path):
+    """cfg5's "tiled per-image, 2 GPUs" at its real size: one 6048x4032 view,
+    9 sources, 8 iterations, split in 2 row bands over 2 ranks (sharing the
+    box's GPU; gloo carries the 23-row halos of src/ACMMP.cu:819-826 after
+    every half-sweep), bit-identical to the unsplit RunPatchMatch."""
+    import time
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    out = str(tmp_path / "cfg5")
+    procs = [ctx.Process(target=_cfg5_worker, args=(r, world, port, out, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=600) for _ in range(world)]
+    for g in got:
+        assert g[0] == "ok", f"rank {g[1]} failed:\n{g[2]}"
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cams, imgs, prm = _cfg5_inputs()
+    with ACMMP(0) as eng:
+        eng.set_params(prm)
+        eng.set_images_device(cams, [im.data_ptr() for im in imgs])
+        t0 = time.perf_counter()
+        eng.RunPatchMatch()
+        dt = time.perf_counter() - t0
+        ref_pl, ref_co = eng.plane_hypotheses(), eng.costs()
+    print(f"cfg5 {CFG5_W}x{CFG5_H}: unsplit {dt:.2f} s incl. D2H; 2 bands on one shared GPU "
+          f"{max(g[2] for g in got):.2f} s incl. gather")
+    assert_bit_exact(np.load(out + "_planes.npy"), ref_pl, "cfg5 planes, 2 bands")
+    assert_bit_exact(np.load(out + "_costs.npy"), ref_co, "cfg5 costs, 2 bands")
+    assert (ref_co < 0.5).mean() > 0.7

@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import gen_cfg4_golden as golden  # noqa: E402
 from test_gpu_distributed import _spawn  # noqa: E402
 from test_gpu_vp_cli import _launch  # noqa: E402
+from parity_util import assert_dmb_trees_equal  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -156,13 +157,7 @@ def test_full_cfg4_cpp_driver_world8_matches_world1(full_cfg4):
     if not os.path.isdir(d + "/F4CPP"):  # the world-1 maps of the test above
         _launch(d, "/F4CPP", 1, "rccl", ["--no_fusion"], timeout=1000)
     _launch(d, "/F4CPP8", 8, "tcp", ["--no_fusion"], timeout=1000)
-    names = ("depths", "depths_geom", "normals", "costs")
-    for v in range(FULL_VIEWS):
-        for name in names:
-            a = os.path.join(aio.result_folder(d + "/F4CPP", v), name + ".dmb")
-            b = os.path.join(aio.result_folder(d + "/F4CPP8", v), name + ".dmb")
-            with open(a, "rb") as fa, open(b, "rb") as fb:
-                assert fa.read() == fb.read(), f"view {v} {name}: world 8 differs from world 1"
+    assert_dmb_trees_equal(d + "/F4CPP8", d + "/F4CPP", range(FULL_VIEWS), "acmmp_main world 8 vs world 1")
 
 
 @pytest.mark.timeout(1200)
@@ -178,10 +173,4 @@ def test_full_cfg4_python_driver_world8_matches_world1(full_cfg4):
     splits = {tuple(got[r][1]) for r in range(8)}
     assert len(splits) == 1 and len(next(iter(splits))) == FULL_VIEWS % 8, got  # the tail view, in 8 bands
     assert sorted(v for r in range(8) for v in got[r][0]) == list(range(FULL_VIEWS))
-    names = ("depths", "depths_geom", "normals", "costs")
-    for v in range(FULL_VIEWS):
-        for name in names:
-            a = os.path.join(aio.result_folder(d + "/F4PY", v), name + ".dmb")
-            b = os.path.join(aio.result_folder(d + "/F4PY8", v), name + ".dmb")
-            with open(a, "rb") as fa, open(b, "rb") as fb:
-                assert fa.read() == fb.read(), f"view {v} {name}: world 8 differs from world 1"
+    assert_dmb_trees_equal(d + "/F4PY8", d + "/F4PY", range(FULL_VIEWS), "acmmp_amd.distributed world 8 vs world 1")
