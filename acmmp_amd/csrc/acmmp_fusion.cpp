@@ -199,18 +199,13 @@ class Pool {
         for (auto &t : workers_) t.join();
     }
     int size() const { return (int)workers_.size(); }
-    std::shared_ptr<Job> submit(int n, std::function<void(int)> fn, bool front = false) {
+    std::shared_ptr<Job> submit(int n, std::function<void(int)> fn) {
         auto j = std::make_shared<Job>();
         j->fn = std::move(fn);
         j->n = n;
         {
             std::lock_guard<std::mutex> g(mu_);
-            if (front) {
-                jobs_.push_front(j);
-                front_gen_.fetch_add(1, std::memory_order_relaxed);
-            } else {
-                jobs_.push_back(j);
-            }
+            jobs_.push_back(j);
         }
         cv_.notify_all();
         return j;
@@ -219,32 +214,16 @@ class Pool {
         std::unique_lock<std::mutex> g(mu_);
         done_cv_.wait(g, [&] { return j->done.load() == j->n; });
     }
-    // fn(0..n-1) ahead of every queued job (workers switch to it after their
-    // current item), the calling thread taking items too; returns when done
-    void run(int n, std::function<void(int)> fn) {
-        if (n <= 0) return;
-        auto j = submit(n, std::move(fn), true);
-        for (int i; (i = j->next.fetch_add(1)) < j->n;) {
-            j->fn(i);
-            if (j->done.fetch_add(1) + 1 == j->n) {
-                std::lock_guard<std::mutex> g(mu_);
-                done_cv_.notify_all();
-            }
-        }
-        wait(j);
-    }
 
   private:
     void loop() {
         for (;;) {
             std::shared_ptr<Job> j;
-            unsigned gen;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return stop_ || !jobs_.empty(); });
                 if (stop_ && jobs_.empty()) return;
                 j = jobs_.front();
-                gen = front_gen_.load(std::memory_order_relaxed);
             }
             int i;
             bool any = false;
@@ -255,7 +234,6 @@ class Pool {
                     std::lock_guard<std::mutex> g(mu_);
                     done_cv_.notify_all();
                 }
-                if (front_gen_.load(std::memory_order_relaxed) != gen) break;  // a priority job arrived
             }
             if (!any) {  // exhausted: retire it from the queue
                 std::lock_guard<std::mutex> g(mu_);
@@ -267,7 +245,6 @@ class Pool {
     std::deque<std::shared_ptr<Job>> jobs_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    std::atomic<unsigned> front_gen_{0};
     bool stop_ = false;
 };
 
@@ -663,355 +640,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         for (size_t i = 0; i < n; ++i) cap += (size_t)cols[i] * rows[i];
         cloud.reserve(cap);
     }
-    // ---------------------------------------------------------------------
-    // Exact parallel approval walk. The serial walk's outcome is a function
-    // of pixel order only: a hit (pixel q, source slot j, source pixel x) is
-    // live iff x was not masked when q read it; a live pixel is approved on
-    // its live hits; a live hit is applied (x masked) at the first approval
-    // a >= q iff no other live hit on slot j comes before a (used_list keeps
-    // one entry per slot, and every approval applies the entries written
-    // since the previous one: src/acmmp_definitions.cpp:966-1030). Within
-    // view i only bits that two or more of its pixels hit ("shared targets")
-    // can be read after being written, so:
-    //   (1) in parallel: liveness against the masks at the view's start,
-    //       shared targets, and the decision of every pixel with no hit on a
-    //       shared target (exact: its reads cannot change during the view);
-    //   (2) serially, only the pixels with a shared hit, in pixel order: such
-    //       a hit is dead iff an earlier live hit on the same target is
-    //       applied before this pixel (an approval in [q_l, min(q, next live
-    //       hit on slot j_l)));
-    //   (3) in parallel: every live hit's applied test against all
-    //       approvals, the masks set, the points emitted in pixel order.
-    // Same points, same order, same masks as the serial walk (tests compare
-    // the PLY byte for byte). Used when no problem lists itself or one source
-    // twice (then one target could sit under two slots or in view i).
-    std::vector<uint8_t> walk_parallel_ok(n, 1);
-    if (const char *e = std::getenv("ACMMP_FUSION_WALK"))
-        if (std::string(e) == "serial") std::fill(walk_parallel_ok.begin(), walk_parallel_ok.end(), 0);
-    for (size_t i = 0; i < n; ++i) {
-        std::vector<int> seen = src_index[i];
-        std::sort(seen.begin(), seen.end());
-        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end() ||
-            std::find(seen.begin(), seen.end(), (int)i) != seen.end())
-            walk_parallel_ok[i] = 0;
-    }
-    std::vector<MaskBits> once(n), twice(n);      // per source view: hit by one / by two or more pixels
-    std::vector<std::vector<uint32_t>> tgt_head(n); // per source view: newest live shared hit record on a target
-    constexpr uint32_t kNone = 0xffffffffu, kWritten = 0xfffffffeu;
-    struct PW {
-        std::vector<uint32_t> rowoff, pixoff, hit_pix, slot_pos, slot_list, slot_off, next_ind_app, rec_prev,
-            rec_hit, dep_app, row_pts;
-        std::vector<uint8_t> live, state, appr, hit_slot;
-        std::vector<size_t> touched;  // (s << 32 | sp) of shared targets given a record
-    } pw;
-    size_t n_dep = 0, n_shared_hits = 0;
-    double pt[4] = {0, 0, 0, 0};  // parallel walk phases: (1a, 1b + next approvals, 2, 3) seconds
-    auto parallel_walk = [&](size_t i, const ViewHits &vh, const std::vector<uint64_t *> &mw,
-                             std::vector<uint8_t> &approved) {
-        const int W = cols[i], H = rows[i];
-        const size_t P = (size_t)W * H;
-        const int ns = std::max(problems[i].num_src_images, 1);
-        const std::vector<int> &srcs = src_index[i];
-        constexpr uint32_t kSpMaskP = (1u << kSpBits) - 1;
-        const int nchunk = std::min(H, 64 * std::max(pool.size() + 1, 1));
-        auto rows_of = [&](int k, int &r0, int &r1) {
-            r0 = (int)((int64_t)H * k / nchunk);
-            r1 = (int)((int64_t)H * (k + 1) / nchunk);
-        };
-        for (int j = 0; j < problems[i].num_src_images; ++j) {
-            const size_t s = (size_t)srcs[(size_t)j];
-            const size_t ps = (size_t)cols[s] * rows[s];
-            if (once[s].w.size() != (ps + 63) / 64) {
-                once[s].assign(ps);
-                twice[s].assign(ps);
-            } else {
-                std::fill(once[s].w.begin(), once[s].w.end(), 0ull);
-                std::fill(twice[s].w.begin(), twice[s].w.end(), 0ull);
-            }
-            if (tgt_head[s].size() != ps) tgt_head[s].assign(ps, kNone);
-        }
-        pw.rowoff.resize((size_t)H + 1);
-        pw.rowoff[0] = 0;
-        for (int r = 0; r < H; ++r) pw.rowoff[(size_t)r + 1] = pw.rowoff[(size_t)r] + (uint32_t)vh.hit[(size_t)r].size();
-        const size_t NH = pw.rowoff[(size_t)H];
-        pw.pixoff.resize(P);
-        pw.hit_pix.resize(NH);
-        pw.live.resize(NH);
-        pw.hit_slot.resize(NH);
-        pw.slot_pos.resize(NH);
-        pw.slot_list.resize(NH);
-        pw.state.assign(P, 0);
-        pw.appr.assign(P, 0);
-        std::vector<uint32_t> cnt((size_t)H * ns, 0);
-        auto fetch_set = [](std::vector<uint64_t> &w, size_t k) -> bool {  // returns the old bit
-            return (__atomic_fetch_or(&w[k >> 6], 1ull << (k & 63), __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
-        };
-        auto getb = [](const uint64_t *w, size_t k) -> bool {
-            return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
-        };
-        auto tp0 = now();
-        // (1a) liveness against the masks at the view's start; shared targets
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r0; r < r1; ++r) {
-                const uint32_t *h = vh.hit[(size_t)r].data();
-                const uint16_t *nhr = vh.nhit[(size_t)r].data();
-                uint32_t g = pw.rowoff[(size_t)r];
-                uint32_t *cr = &cnt[(size_t)r * ns];
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c;
-                    const int nh = nhr[c];
-                    if (nh == 0xffff) continue;
-                    pw.pixoff[pc] = g;
-                    const bool skip = masks[i].get(pc);
-                    pw.state[pc] = skip ? 0 : 1;
-                    for (int q = 0; q < nh; ++q, ++g) {
-                        const uint32_t j = h[g - pw.rowoff[(size_t)r]] >> kSpBits, sp = h[g - pw.rowoff[(size_t)r]] & kSpMaskP;
-                        pw.hit_pix[g] = (uint32_t)pc;
-                        pw.hit_slot[g] = (uint8_t)j;
-                        const bool lv = !skip && !getb(mw[j], sp);
-                        pw.live[g] = lv;
-                        if (!lv) continue;
-                        cr[j]++;
-                        const size_t s = (size_t)srcs[j];
-                        if (fetch_set(once[s].w, sp)) fetch_set(twice[s].w, sp);
-                    }
-                }
-            }
-        });
-        auto tp1 = now();
-        pt[0] += secs(tp0, tp1);
-        // slot lists: every live hit of slot j in pixel order (rows, then pixels)
-        pw.slot_off.assign((size_t)ns + 1, 0);
-        std::vector<uint32_t> off((size_t)H * ns);
-        {
-            uint32_t acc = 0;
-            for (int j = 0; j < ns; ++j) {
-                pw.slot_off[(size_t)j] = acc;
-                for (int r = 0; r < H; ++r) {
-                    off[(size_t)r * ns + j] = acc;
-                    acc += cnt[(size_t)r * ns + j];
-                }
-            }
-            pw.slot_off[(size_t)ns] = acc;
-        }
-        // (1b) decisions of the pixels without a shared hit; slot lists
-        const float scal = consistency_scalar;
-        auto decide = [&](size_t pc, int nh, uint32_t g0, float presum) -> bool {
-            int nlive = 0;
-            for (int q = 0; q < nh; ++q) nlive += pw.live[g0 + q];
-            float dyn = presum;
-            if (nlive != nh) {
-                dyn = 0;
-                const uint32_t r = (uint32_t)(pc / W);
-                const float *hx = vh.ex[r].data() + (g0 - pw.rowoff[r]);
-                for (int q = 0; q < nh; ++q)
-                    if (pw.live[g0 + q]) dyn += hx[q];
-            }
-            return nlive >= con_num_thresh && (dyn > scal * nlive);
-        };
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r0; r < r1; ++r) {
-                const uint32_t *h = vh.hit[(size_t)r].data();
-                const uint16_t *nhr = vh.nhit[(size_t)r].data();
-                const float *sumr = vh.sum[(size_t)r].data();
-                uint32_t *o = &off[(size_t)r * ns];
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c;
-                    const int nh = nhr[c];
-                    if (nh == 0xffff || pw.state[pc] == 0) continue;
-                    const uint32_t g0 = pw.pixoff[pc];
-                    bool dep = false;
-                    for (int q = 0; q < nh; ++q) {
-                        const uint32_t g = g0 + q;
-                        if (!pw.live[g]) continue;
-                        const uint32_t hv = h[g - pw.rowoff[(size_t)r]];
-                        const uint32_t j = hv >> kSpBits, sp = hv & kSpMaskP;
-                        const uint32_t at = o[j]++;
-                        pw.slot_list[at] = g;
-                        pw.slot_pos[g] = at;
-                        dep = dep || twice[(size_t)srcs[j]].get(sp);
-                    }
-                    if (dep) pw.state[pc] = 2;
-                    else pw.appr[pc] = decide(pc, nh, g0, sumr[c]);
-                }
-            }
-        });
-        // first approval among the pixels decided so far at or after p (P: none)
-        pw.next_ind_app.resize(P + 1);
-        pw.next_ind_app[P] = (uint32_t)P;
-        std::vector<uint32_t> row_first((size_t)H + 1, (uint32_t)P);
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r1 - 1; r >= r0; --r) {
-                uint32_t nxt = (uint32_t)P;
-                for (int c = W - 1; c >= 0; --c) {
-                    const size_t pc = (size_t)r * W + c;
-                    if (pw.appr[pc]) nxt = (uint32_t)pc;
-                    pw.next_ind_app[pc] = nxt;
-                }
-                row_first[(size_t)r] = nxt;
-            }
-        });
-        for (int r = H - 1; r >= 0; --r)  // carry from the rows below
-            if (row_first[(size_t)r] == (uint32_t)P) row_first[(size_t)r] = row_first[(size_t)r + 1];
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r0; r < r1; ++r) {
-                const uint32_t below = row_first[(size_t)r + 1];
-                for (int c = W - 1; c >= 0 && pw.next_ind_app[(size_t)r * W + c] == (uint32_t)P; --c)
-                    pw.next_ind_app[(size_t)r * W + c] = below;
-            }
-        });
-        // approvals in [a, b): the independent ones, or the dependent ones so far (sorted)
-        pw.dep_app.clear();
-        auto approval_in = [&](uint32_t a, uint32_t b) -> bool {
-            if (a >= b) return false;
-            if (pw.next_ind_app[a] < b) return true;
-            if (b - a <= 16) {  // every pixel in [a, b) is decided: read the flags
-                for (uint32_t t = a; t < b; ++t)
-                    if (pw.appr[t]) return true;
-                return false;
-            }
-            auto it = std::lower_bound(pw.dep_app.begin(), pw.dep_app.end(), a);
-            return it != pw.dep_app.end() && *it < b;
-        };
-        // pixel of the next live hit on the slot of hit g (P: none)
-        auto next_live_pix = [&](uint32_t g, uint32_t j) -> uint32_t {
-            const uint32_t end = pw.slot_off[(size_t)j + 1];
-            for (uint32_t t = pw.slot_pos[g] + 1; t < end; ++t)
-                if (pw.live[pw.slot_list[t]]) return pw.hit_pix[pw.slot_list[t]];
-            return (uint32_t)P;
-        };
-        auto tp2 = now();
-        pt[1] += secs(tp1, tp2);
-        // (2) the pixels with a shared hit, serially in pixel order
-        pw.rec_prev.clear();
-        pw.rec_hit.clear();
-        pw.touched.clear();
-        size_t ndep = 0;
-        for (int r = 0; r < H; ++r) {
-            const uint32_t *h = vh.hit[(size_t)r].data();
-            const uint16_t *nhr = vh.nhit[(size_t)r].data();
-            const float *sumr = vh.sum[(size_t)r].data();
-            const uint32_t ro = pw.rowoff[(size_t)r];
-            for (int c = 0; c < W; ++c) {
-                const size_t pc = (size_t)r * W + c;
-                if (pw.state[pc] != 2) continue;
-                ++ndep;
-                const int nh = nhr[c];
-                const uint32_t g0 = pw.pixoff[pc];
-                for (int q = 0; q < nh; ++q) {
-                    const uint32_t g = g0 + q;
-                    if (!pw.live[g]) continue;
-                    const uint32_t hv = h[g - ro];
-                    const size_t s = (size_t)srcs[hv >> kSpBits];
-                    const uint32_t sp = hv & kSpMaskP;
-                    if (!twice[s].get(sp)) continue;
-                    uint32_t &head = tgt_head[s][sp];
-                    if (head == kWritten) {
-                        pw.live[g] = 0;
-                        continue;
-                    }
-                    for (uint32_t rec = head; rec != kNone; rec = pw.rec_prev[rec]) {
-                        const uint32_t gl = pw.rec_hit[rec];
-                        const uint32_t ql = pw.hit_pix[gl];
-                        const uint32_t jl = pw.hit_slot[gl];
-                        const uint32_t t = std::min<uint32_t>((uint32_t)pc, next_live_pix(gl, jl));
-                        if (approval_in(ql, t)) {  // written before this pixel: stays written
-                            head = kWritten;
-                            pw.live[g] = 0;
-                            break;
-                        }
-                    }
-                }
-                // this pixel's live shared hits join their targets' chains
-                for (int q = 0; q < nh; ++q) {
-                    const uint32_t g = g0 + q;
-                    if (!pw.live[g]) continue;
-                    const uint32_t hv = h[g - ro];
-                    const size_t s = (size_t)srcs[hv >> kSpBits];
-                    const uint32_t sp = hv & kSpMaskP;
-                    if (!twice[s].get(sp)) continue;
-                    uint32_t &head = tgt_head[s][sp];
-                    if (head == kNone) pw.touched.push_back(s << 32 | sp);
-                    pw.rec_prev.push_back(head);
-                    pw.rec_hit.push_back(g);
-                    head = (uint32_t)(pw.rec_hit.size() - 1);
-                }
-                if (decide(pc, nh, g0, sumr[c])) {
-                    pw.appr[pc] = 1;
-                    pw.dep_app.push_back((uint32_t)pc);
-                }
-            }
-        }
-        n_dep += ndep;
-        n_shared_hits += pw.rec_hit.size();
-        for (size_t t : pw.touched) tgt_head[t >> 32][t & 0xffffffffu] = kNone;
-        auto tp3 = now();
-        pt[2] += secs(tp2, tp3);
-        // (3) applied hits -> masks; points in pixel order
-        pw.row_pts.assign((size_t)H + 1, 0);
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r0; r < r1; ++r) {
-                const uint32_t *h = vh.hit[(size_t)r].data();
-                const uint16_t *nhr = vh.nhit[(size_t)r].data();
-                const uint32_t ro = pw.rowoff[(size_t)r];
-                uint32_t npts = 0;
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c;
-                    const int nh = nhr[c];
-                    if (nh == 0xffff || pw.state[pc] == 0) continue;
-                    npts += pw.appr[pc];
-                    const uint32_t g0 = pw.pixoff[pc];
-                    for (int q = 0; q < nh; ++q) {
-                        const uint32_t g = g0 + q;
-                        if (!pw.live[g]) continue;
-                        const uint32_t hv = h[g - ro];
-                        const uint32_t j = hv >> kSpBits, sp = hv & kSpMaskP;
-                        if (!approval_in((uint32_t)pc, next_live_pix(g, j))) continue;
-                        const size_t s = (size_t)srcs[j];
-                        __atomic_fetch_or(&masks[s].w[sp >> 6], 1ull << (sp & 63), __ATOMIC_RELAXED);
-                        if (write_debug_images) {
-                            const int ux = (int)(sp % (uint32_t)cols[s]), uy = (int)(sp / (uint32_t)cols[s]);
-                            if (uy < H && ux < W) __atomic_store_n(&approved[(size_t)uy * W + ux], (uint8_t)255, __ATOMIC_RELAXED);
-                        }
-                    }
-                }
-                pw.row_pts[(size_t)r + 1] = npts;
-            }
-        });
-        for (int r = 0; r < H; ++r) pw.row_pts[(size_t)r + 1] += pw.row_pts[(size_t)r];
-        const size_t base = cloud.size();
-        cloud.resize(base + pw.row_pts[(size_t)H]);
-        pool.run(nchunk, [&](int k) {
-            int r0, r1;
-            rows_of(k, r0, r1);
-            for (int r = r0; r < r1; ++r) {
-                size_t at = base + pw.row_pts[(size_t)r];
-                for (int c = 0; c < W; ++c) {
-                    const size_t pc = (size_t)r * W + c;
-                    if (!pw.appr[pc]) continue;
-                    const float ref_depth = depths[i][pc];
-                    const float *ref_normal = &normals[i][pc * 3];
-                    const uint8_t *bgr = &images[i][pc * 3];
-                    Point &p = cloud[at++];
-                    p.coord = world_point(c, r, ref_depth, cameras[i]);
-                    p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
-                    p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
-                }
-            }
-        });
-        for (size_t pc = 0; pc < P; ++pc) n_live += pw.state[pc] != 0;
-        pt[3] += secs(tp3, now());
-    };
     const auto t_loaded = now();
     auto job = start_phase1(0);
     for (size_t i = 0; i < n; ++i) {
@@ -1027,9 +655,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         // per source: its mask words; used_list as mask indices (-1 unset)
         std::vector<uint64_t *> mw((size_t)std::max(num_ngb, 1));
         for (int j = 0; j < num_ngb; ++j) mw[(size_t)j] = masks[(size_t)src_index[i][j]].w.data();
-        if (walk_parallel_ok[i]) {
-            parallel_walk(i, vh, mw, approved);
-        } else {
         std::vector<int64_t> used_sp((size_t)std::max(num_ngb, 1), -1);
         uint32_t dirty = 0;  // used_sp entries written since the last approval
         auto bit = [](const uint64_t *w, size_t k) -> bool {
@@ -1111,7 +736,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 }
             }
         }
-        }  // serial walk
         t_walk += secs(t1, now());
         if (write_debug_images) {
             const std::string dbg = dense + "/approved_pixels_cam_" + std::to_string(i) + ".png";
@@ -1127,10 +751,9 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     if (timing)
         std::fprintf(stderr,
                      "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d "
-                     "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu pinned=%d "
-                     "shared_target_pixels=%zu shared_hits=%zu pw_phases=%.2f/%.2f/%.2f/%.2fs\n",
+                     "walked_pixels=%zu hits=%zu pixels_with_masked_hits=%zu points=%zu pinned=%d\n",
                      secs(t_start, t_loaded), t_wait, t_walk, secs(t_walked, now()), pool.size() + 1, n_live,
-                     n_hits, n_masked, cloud.size(), (int)dom.pinned(), n_dep, n_shared_hits, pt[0], pt[1], pt[2], pt[3]);
+                     n_hits, n_masked, cloud.size(), (int)dom.pinned());
     return rc;
 }
 
