@@ -38,7 +38,10 @@ constexpr int kTaps = 6;
 // 16 x 16 blocks of four 8 x 8-pixel waves, candidate planes staged in LDS,
 // refinement items packed across lanes, two software-pipelined patch rows,
 // packed-pair u8 lerps, view selection in registers, 2 waves per SIMD.
-constexpr int kWaveRows = 8;   // rows of pixels per wave (lane_geom_of)
+#ifndef ACMMP_WAVE_ROWS
+#define ACMMP_WAVE_ROWS 8
+#endif
+constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geom_of; A/B builds only)
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
 
 // ----------------------------------------------------------------- textures
@@ -854,7 +857,24 @@ DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     constexpr int R = kWaveRows, C = 64 / R, WPR = kBX / C;
     static_assert(kBX % C == 0 && kBY % R == 0, "2D wave map");
     const int w = tid >> 6, l = tid & 63;
-    const int tx = (w % WPR) * C + (l % C), ty = (w / WPR) * R + l / C;
+#ifndef ACMMP_LANE_MAP
+#define ACMMP_LANE_MAP 0
+#endif
+    int lc, lr;  // lane -> (column, row) inside the wave's C x R pixels
+    if (ACMMP_LANE_MAP == 1 && C == 8 && R == 8) {  // 16-lane groups of 4 x 4, row-major inside
+        lc = (l & 3) + 4 * ((l >> 4) & 1);
+        lr = ((l >> 2) & 3) + 4 * (l >> 5);
+    } else if (ACMMP_LANE_MAP == 2 && C == 8 && R == 8) {  // 16-lane groups of 4 x 4, column-major inside
+        lc = ((l >> 2) & 3) + 4 * ((l >> 4) & 1);
+        lr = (l & 3) + 4 * (l >> 5);
+    } else if (ACMMP_LANE_MAP == 3 && C == 8 && R == 8) {  // 16-lane groups of 8 x 2, column-major inside
+        lc = (l >> 1) & 7;
+        lr = (l & 1) + 2 * (l >> 4);
+    } else {
+        lc = l % C;
+        lr = l / C;
+    }
+    const int tx = (w % WPR) * C + lc, ty = (w / WPR) * R + lr;
     g.k = b.bx * kBX + tx;
     g.py = b.by * kBY + ty;
     g.s = (g.py + colour) & 1;

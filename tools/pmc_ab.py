@@ -38,3 +38,8 @@ for d in sys.argv[1:]:
               f"  VMEM {c['SQ_ACTIVE_INST_VMEM'] / wc:.3f}  wait_any {c['SQ_WAIT_ANY'] / wc:.3f}  wait_inst {c['SQ_WAIT_INST_ANY'] / wc:.3f}")
     print(f"   TD busy {c.get('TD_TD_BUSY_sum', 0) / (gui * 256):.3f}  TA busy {c.get('TA_TA_BUSY_sum', 0) / (gui * 256):.3f}"
           f"  LDS conflict/idx {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_LDS_IDX_ACTIVE', 1), 1):.3f}")
+    tw = c.get("TA_BUFFER_READ_WAVEFRONTS_sum", 0)
+    if tw and "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+        print(f"   per buffer-read wave-instruction: TD cycles {c.get('TD_TD_BUSY_sum', 0) / tw:.2f}"
+              f"  TCP accesses {c['TCP_TOTAL_CACHE_ACCESSES_sum'] / tw:.2f}"
+              f"  L1 misses to L2 {c.get('TCP_TCC_READ_REQ_sum', 0) / tw:.2f}")
