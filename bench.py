@@ -250,62 +250,70 @@ def main():
 
 
 def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
-    """The dominant kernel's roofline (k_sweep, >90 % of the step's GPU time).
-
-    k_sweep is bound by the texture-data (TD) path that serves its
-    buffer_load gathers, so the binding roofline is that
-    unit's: achieved = gather wave-instructions per second, peak = the rate
-    at which the TD would be 100 % busy at the measured TD cycles per
-    instruction (256 CUs x clock / cycles per instruction), frac = TD busy
-    fraction. The HBM roofline is reported beside it from the memory-side
-    counter bytes. Durations: the un-overlapped HIP-event time of one launch
-    (iso_ms, one stream); rocprofv3's profiled duration is in `pmc`."""
+    """The dominant kernel's roofline (k_sweep, >90 % of the step's GPU time),
+    in the contract's form: bound "hbm", achieved = ALGORITHMIC bytes per
+    launch (SURVEY §8d's gather-byte model: every NCC sample's texels counted
+    as if uncached) / launch time, peak = 8 TB/s, traffic = the HBM bytes the
+    PMC counters see per launch. The model counts L1-served gathers, so frac
+    exceeds 1 and `traffic` is far below the algorithmic bytes: the kernel is
+    not HBM-bound. What binds it is reported beside it: the texture-data (TD)
+    path that serves the gathers (`binding_unit`: TD busy fraction, one TD
+    cycle per L1 cache access, profiles/r04_td_addressing.md), the VALU
+    (`valu`) and the physical HBM fraction (`hbm_physical`). Durations: the
+    un-overlapped HIP-event time of one launch (iso_ms, one stream);
+    rocprofv3's profiled duration is in `pmc`."""
+    achieved = logical_bytes / (iso_ms / 1e3) / 1e9
     out = {
-        "bound": "td-gather",
+        "bound": "hbm",
         "kernel": "k_sweep (CheckerboardPropagation)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "algorithmic_bytes_per_launch": round(logical_bytes),
+        "model": "SURVEY §8d / BASELINE.md §3: per pixel-iteration 14 (N-1) NCC x 724 B + 572 B state "
+                 "(+ 14 (N-1) x 4 B geometric), P/2 pixels per launch, photometric/geometric mean; "
+                 "frac > 1 = served from L1, not HBM",
         "launch_ms": round(iso_ms, 3),
         "launch_ms_note": "HIP events on the engine stream, one launch alone (one photometric + one geometric "
                           "view on one stream after the timed region); in the timed region "
                           f"{streams} views share the GPU and a launch spans "
                           f"{timed_ms / max(timed_launches, 1):.3f} ms",
-        "logical_gather_GBs": round(logical_bytes / (iso_ms / 1e3) / 1e9, 1),
-        "logical_note": "SURVEY §8d / BASELINE.md §3 model (36 samples x 5 texels x 4 B per NCC, counted as if "
-                        "uncached) per launch / launch_ms: a data-volume figure, not an HBM fraction",
     }
     if not pmc or "error" in pmc:
-        out.update({"achieved": None, "peak": None, "unit": "Ginst/s", "frac": None, "traffic": None,
-                    "pmc": (pmc or {}).get("error", "counter passes skipped")})
+        out["pmc"] = (pmc or {}).get("error", "counter passes skipped")
         return out
     clock_hz = pmc["clock_ghz"] * 1e9
     insts = pmc["gather_insts"]
-    achieved = insts / (iso_ms / 1e3) / 1e9
-    peak = 256 * clock_hz / pmc["td_cyc_per_inst"] / 1e9
     hbm_gbs = pmc["hbm_bytes"] / (iso_ms / 1e3) / 1e9
     out.update({
-        "achieved": round(achieved, 2),
-        "peak": round(peak, 2),
-        "unit": "Ginst/s",
-        "frac": round(pmc["td_busy_frac"], 4),
         "traffic": round(pmc["hbm_bytes"]),
-        "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per launch / launch_ms; peak = 256 CUs x clock "
-                 "(GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / TA_BUFFER_READ_WAVEFRONTS_sum); "
-                 "frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8)",
-        "hbm": {
-            "bound": "hbm",
+        "traffic_note": "(2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 (Infinity-Cache "
+                        "hits included), FETCH doubled per the gfx950 calibration",
+        "hbm_physical": {
             "achieved": round(hbm_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
-            "traffic": round(pmc["hbm_bytes"]),
-            "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 "
-                    "(Infinity-Cache hits included), FETCH doubled per the gfx950 calibration",
+        },
+        "binding_unit": {
+            "bound": "td-gather",
+            "achieved": round(insts / (iso_ms / 1e3) / 1e9, 2),
+            "peak": round(256 * clock_hz / pmc["td_cyc_per_inst"] / 1e9, 2),
+            "unit": "Ginst/s",
+            "frac": round(pmc["td_busy_frac"], 4),
+            "td_cycles_per_gather": round(pmc["td_cyc_per_inst"], 2),
+            "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per launch / launch_ms; peak = 256 CUs x clock "
+                     "(GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / TA_BUFFER_READ_WAVEFRONTS_sum); "
+                     "frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8)",
         },
         "valu": {
             "bound": "valu",
             "frac": round(pmc["valu_busy_frac"], 4),
             "insts": round(pmc["valu_insts"]),
             "note": "share of SIMD cycles issuing VALU (4 x SQ_ACTIVE_INST_VALU quad-cycles / (1024 SIMDs x "
-                    "GRBM_GUI_ACTIVE/8)): the kernel is co-bound by the TD gather path (frac) and the VALU",
+                    "GRBM_GUI_ACTIVE/8))",
         },
         "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
     })

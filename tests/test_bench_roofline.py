@@ -35,8 +35,13 @@ def test_bench_roofline_block():
     import bench
     s = bench_pmc.summarize(_passes())
     r = bench.roofline(s, 4.0, 1.0e10, 8.0, 2, 2)
-    assert r["bound"] == "td-gather" and 0 < r["frac"] <= 1
+    # the contract's form: algorithmic bytes / launch time against the HBM peak
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
+    assert abs(r["achieved"] - 1.0e10 / 4.0e-3 / 1e9) < 0.1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["traffic"] == s["hbm_bytes"]
+    assert r["binding_unit"]["bound"] == "td-gather" and 0 < r["binding_unit"]["frac"] <= 1
     assert r["valu"]["bound"] == "valu" and r["valu"]["frac"] == round(s["valu_busy_frac"], 4)
-    assert r["hbm"]["frac"] < 1
+    assert r["hbm_physical"]["frac"] < 1
     for k in ("achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
