@@ -569,7 +569,20 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         if ((size_t)cols[i] * rows[i] > (size_t(1) << kSpBits) || problems[i].num_src_images > 32)
             return ffail(ACMMP_ERR_ARG, "view %d: fusion supports images up to 2^27 pixels and 32 sources",
                          problems[i].ref_image_id);
+    // Source-major inside a row: every live pixel's world point first, then
+    // one source at a time over the row (its depth/normal/mask reads follow
+    // the row's projection into that source instead of hopping between 20
+    // sources per pixel), then each pixel's hits in ascending j as the
+    // reference adds them (same values, same order).
+    struct RowScratch {
+        std::vector<F3> X;
+        std::vector<int> live;           // columns of the live pixels
+        std::vector<uint32_t> sp;        // [live k][j]: source pixel of a hit, or kNoHit
+        std::vector<float> e;            // [live k][j]: its exp(-tmp_index)
+    };
+    constexpr uint32_t kNoHit = 0xffffffffu;
     auto phase1 = [&](size_t i, ViewHits &vh, int r) {
+        thread_local RowScratch rs;
         const int W = cols[i];
         const int num_ngb = problems[i].num_src_images;
         const float depth_max = cameras[i].depth_max;
@@ -581,47 +594,69 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         hx.clear();
         nh.assign((size_t)W, 0xffff);
         sum.assign((size_t)W, 0.0f);
+        rs.live.clear();
+        rs.X.clear();
         for (int c = 0; c < W; ++c) {
             const size_t pc = (size_t)r * W + c;
             if (masks[i].get(pc)) continue;
             const float ref_depth = depths[i][pc];
-            const float *ref_normal = &normals[i][pc * 3];
             if (ref_depth <= 0.0 || ref_depth >= depth_max) continue;
-            const F3 PointX = world_point(c, r, ref_depth, cameras[i]);
+            rs.live.push_back(c);
+            rs.X.push_back(world_point(c, r, ref_depth, cameras[i]));
+        }
+        const size_t nl = rs.live.size();
+        const size_t nj = (size_t)std::max(num_ngb, 1);
+        rs.sp.assign(nl * nj, kNoHit);
+        rs.e.resize(nl * nj);
+        for (int j = 0; j < num_ngb; ++j) {
+            const int s = src_index[i][j];
+            const int src_cols = cols[s], src_rows = rows[s];
+            for (size_t k = 0; k < nl; ++k) {
+                const int c = rs.live[k];
+                const size_t pc = (size_t)r * W + c;
+                const float ref_depth = depths[i][pc];
+                const float *ref_normal = &normals[i][pc * 3];
+                float ptx, pty, proj_depth;
+                project(rs.X[k], cameras[s], ptx, pty, proj_depth);
+                const int src_r = int(pty + 0.5f);
+                const int src_c = int(ptx + 0.5f);
+                if (!(src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows)) continue;
+                const size_t sp = (size_t)src_r * src_cols + src_c;
+                if (masks[s].get(sp)) continue;
+                const float src_depth = depths[s][sp];
+                const float *src_normal = &normals[s][sp * 3];
+                if (src_depth <= 0.0) continue;
+                const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
+                float tx, ty;
+                project(tmp_X, cameras[i], tx, ty, proj_depth);
+                // std::pow(v, 2) of a float v is exact in double: v * v
+                const double dx = (double)(c - tx), dy = (double)(r - ty);
+                const float reproj_error = (float)std::sqrt(dx * dx + dy * dy);
+                const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
+                // the reference evaluates all three before the test; acos is
+                // pure, so it is only needed where the first two pass
+                if (!(reproj_error < 2.0f && relative_depth_diff < 0.01f)) continue;
+                const float angle = get_angle(ref_normal, src_normal);
+                if (angle < 0.174533f) {
+                    const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
+                    rs.sp[k * nj + (size_t)j] = (uint32_t)sp;
+                    rs.e[k * nj + (size_t)j] = std::exp(-tmp_index);
+                }
+            }
+        }
+        for (size_t k = 0; k < nl; ++k) {
             const size_t k0 = h.size();
             float total = 0;
             for (int j = 0; j < num_ngb; ++j) {
-                const int s = src_index[i][j];
-                const int src_cols = cols[s], src_rows = rows[s];
-                float ptx, pty, proj_depth;
-                project(PointX, cameras[s], ptx, pty, proj_depth);
-                const int src_r = int(pty + 0.5f);
-                const int src_c = int(ptx + 0.5f);
-                if (src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows) {
-                    const size_t sp = (size_t)src_r * src_cols + src_c;
-                    if (masks[s].get(sp)) continue;
-                    const float src_depth = depths[s][sp];
-                    const float *src_normal = &normals[s][sp * 3];
-                    if (src_depth <= 0.0) continue;
-                    const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
-                    float tx, ty;
-                    project(tmp_X, cameras[i], tx, ty, proj_depth);
-                    // std::pow(v, 2) of a float v is exact in double: v * v
-                    const double dx = (double)(c - tx), dy = (double)(r - ty);
-                    const float reproj_error = (float)std::sqrt(dx * dx + dy * dy);
-                    const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
-                    const float angle = get_angle(ref_normal, src_normal);
-                    if (reproj_error < 2.0f && relative_depth_diff < 0.01f && angle < 0.174533f) {
-                        const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                        const float e = std::exp(-tmp_index);
-                        h.push_back((uint32_t)j << kSpBits | (uint32_t)sp);
-                        hx.push_back(e);
-                        total += e;
-                    }
-                }
+                const uint32_t sp = rs.sp[k * nj + (size_t)j];
+                if (sp == kNoHit) continue;
+                const float e = rs.e[k * nj + (size_t)j];
+                h.push_back((uint32_t)j << kSpBits | sp);
+                hx.push_back(e);
+                total += e;
             }
-            nh[(size_t)c] = (uint16_t)(h.size() - k0);
-            sum[(size_t)c] = total;
+            nh[(size_t)rs.live[k]] = (uint16_t)(h.size() - k0);
+            sum[(size_t)rs.live[k]] = total;
         }
     };
     std::vector<ViewHits> vhits(2);
