@@ -35,7 +35,8 @@ constexpr int kTaps = 6;
 
 // The kernel shapes below are the measured winners of the A/B experiments
 // recorded in DESIGN.md §4 (the rejected variants live in git history only):
-// 16 x 16 blocks of four 8 x 8-pixel waves, candidate planes staged in LDS,
+// 16 x 16 blocks of four 8 x 8-pixel waves (lanes column-major in 4 x 4
+// quarters, lane_geom_of), candidate planes staged in LDS,
 // refinement items packed across lanes, two software-pipelined patch rows,
 // packed-pair u8 lerps, view selection in registers, 2 waves per SIMD.
 #ifndef ACMMP_WAVE_ROWS
@@ -447,7 +448,7 @@ struct RowFetch {
 
 // Projection, clamp, fractions and record index of patch row jj, and its 6
 // loads issued (not waited for).
-template <bool FAST, int TX, bool EASY = false>
+template <bool FAST, int TX>
 DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
                    RowFetch<TX> &rf) {
     constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
@@ -467,19 +468,14 @@ DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v 
             inv = f2v{1.0f / hz.x, 1.0f / hz.y};
         }
         f2v u = hx * inv, v = hy * inv;
-        if (!EASY) {  // EASY: proven the identity for the whole patch (bilateral_ncc)
-            u = (u + 0.5f) - 0.5f;
-            v = (v + 0.5f) - 0.5f;
-        }
+        u = (u + 0.5f) - 0.5f;
+        v = (v + 0.5f) - 0.5f;
         // clamp to [-1, W] x [-1, H]. FAST: every value is finite or +-inf
         // (finite homography, |hz| inside the reciprocal window), where
         // v_med3 equals max-then-min. Otherwise v_max/v_min (NaN -> -1;
         // bounds are never +-0) == the oracle's selects.
         f2v xs, ys;
-        if (EASY) {  // every sample inside [1, W] x [1, H]: the clamp is the identity
-            xs = u;
-            ys = v;
-        } else if (FAST) {
+        if (FAST) {
             xs = f2v{__builtin_amdgcn_fmed3f(u.x, -1.0f, fw.x), __builtin_amdgcn_fmed3f(u.y, -1.0f, fw.x)};
             ys = f2v{__builtin_amdgcn_fmed3f(v.x, -1.0f, fh.x), __builtin_amdgcn_fmed3f(v.y, -1.0f, fh.x)};
         } else {
@@ -588,7 +584,7 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
 // (src/ACMMP.cu:382-412). The row loop is software-pipelined: row jj + 1's
 // loads are issued before row jj is reduced, so a row's gather latency
 // overlaps the previous row's arithmetic.
-template <bool FAST, int TX, bool EASY = false>
+template <bool FAST, int TX>
 DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, const float *rt, int wstride, int px,
                        int py, float &sum_src, float &sum_ss, float &sum_rs) {
     f2v cx[kPairs], cy[kPairs], cz[kPairs];
@@ -604,12 +600,12 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
     // two rows per trip (ping-pong fetch buffers, no register copies)
     RowFetch<TX> ra, rb;
-    fetch_row<FAST, TX, EASY>(im, H, cx, cy, cz, py, 0, ra);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
 #pragma unroll 1
     for (int jj = 0; jj < kTaps; jj += 2) {
-        fetch_row<FAST, TX, EASY>(im, H, cx, cy, cz, py, jj + 1, rb);
+        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 1, rb);
         reduce_row<TX>(ra, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
-        if (jj + 2 < kTaps) fetch_row<FAST, TX, EASY>(im, H, cx, cy, cz, py, jj + 2, ra);
+        if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 2, ra);
         reduce_row<TX>(rb, wl, rt, wstride, jj + 1, acc_s, acc_ss, acc_rs);
     }
     sum_src = 0.0f;
@@ -628,7 +624,7 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // returns the three weighted sums (ncc_sums_rows above).
-template <bool FAST, int TX, bool EASY = false>
+template <bool FAST, int TX>
 DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
                   float &sum_ss, float &sum_rs) {
     // re-read weights from LDS each call rather than caching them in VGPRs
@@ -637,7 +633,7 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
     const WSlot *wl = pp.w - pp.wo + wo;
-    ncc_sums_rows<FAST, TX, EASY>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
@@ -669,47 +665,7 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-#ifndef ACMMP_EASY_PATCH
-#define ACMMP_EASY_PATCH 0
-#endif
-    bool easy = false;
-    if (ACMMP_EASY_PATCH && fast) {
-        // Pin P2's (u + 0.5) - 0.5 and the [-1, W] x [-1, H] clamp are both
-        // the identity for every sample when the patch's coordinates lie in
-        // [1, W] x [1, H] and u, u + 0.5 share a binade (then u + 0.5 is
-        // exact: 0.5 is a multiple of ulp(u) for 1 <= u < 2^23). The
-        // projective map sends the sample grid's corners to the extremes of
-        // its image (hz keeps one sign: `fast`), so the four corners bound
-        // every sample; the margin m covers the corners' approximate
-        // reciprocal and the samples' own rounding (a few ulps, < 2^-10 of
-        // u below 8192).
-        const f2v xc = f2v{xl, xr};
-        f2v ut, ub, vt, vb;
-        {
-            const f2v hxt = fma2(splat(H[1]), splat(yt), fma2(splat(H[0]), xc, splat(H[2])));
-            const f2v hyt = fma2(splat(H[4]), splat(yt), fma2(splat(H[3]), xc, splat(H[5])));
-            const f2v hxb = fma2(splat(H[1]), splat(yb), fma2(splat(H[0]), xc, splat(H[2])));
-            const f2v hyb = fma2(splat(H[4]), splat(yb), fma2(splat(H[3]), xc, splat(H[5])));
-            const f2v it = f2v{__builtin_amdgcn_rcpf(z00), __builtin_amdgcn_rcpf(z10)};
-            const f2v ib = f2v{__builtin_amdgcn_rcpf(z01), __builtin_amdgcn_rcpf(z11)};
-            ut = hxt * it;
-            vt = hyt * it;
-            ub = hxb * ib;
-            vb = hyb * ib;
-        }
-        const float m = 1.0f / 64.0f;
-        const float ulo = fminf(fminf(ut.x, ut.y), fminf(ub.x, ub.y)) - m;
-        const float uhi = fmaxf(fmaxf(ut.x, ut.y), fmaxf(ub.x, ub.y)) + m;
-        const float vlo = fminf(fminf(vt.x, vt.y), fminf(vb.x, vb.y)) - m;
-        const float vhi = fmaxf(fmaxf(vt.x, vt.y), fmaxf(vb.x, vb.y)) + m;
-        const float uh = uhi + 0.5f, vh = vhi + 0.5f;
-        easy = ulo >= 1.0f && vlo >= 1.0f && uhi <= (float)im.W && vhi <= (float)im.H && uh < 8192.0f &&
-               vh < 8192.0f && (__float_as_uint(ulo) >> 23) == (__float_as_uint(uh) >> 23) &&
-               (__float_as_uint(vlo) >> 23) == (__float_as_uint(vh) >> 23);
-    }
-    if (ACMMP_EASY_PATCH && __ballot(easy) == __ballot(1))  // wave-uniform: one copy of the loop runs
-        ncc_sums<true, TX, true>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-    else if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     sum_src *= pp.inv_wsum;
     const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
@@ -902,19 +858,24 @@ DEV LaneGeom lane_geom_of(int colour, BlockXY b, int tid) {
     constexpr int R = kWaveRows, C = 64 / R, WPR = kBX / C;
     static_assert(kBX % C == 0 && kBY % R == 0, "2D wave map");
     const int w = tid >> 6, l = tid & 63;
+    // Which pixel of its C x R patch each lane takes. A gather costs one TD
+    // cycle per L1 access, and an access serves one 64-B line for one group
+    // of 8 lanes: the even or the odd lanes of a 16-lane quarter-wave
+    // (profiles/r04_td_addressing.md). Default (lane map 2): a quarter is 4
+    // columns x 4 rows, lanes column-major inside, so each 8-lane group is 4
+    // adjacent colour-split columns of 2 rows (rows r, r + 2): 36 accesses
+    // per k_sweep gather against 46 for row-major lanes (8 columns x 2 rows
+    // per quarter, groups of every other column), bench +2 %
+    // (profiles/r04_lanemap2_pmc.txt). ACMMP_LANE_MAP=0 restores row-major
+    // lanes for A/B builds. Each lane still computes its own pixel, so the
+    // map changes no result.
 #ifndef ACMMP_LANE_MAP
-#define ACMMP_LANE_MAP 0
+#define ACMMP_LANE_MAP 2
 #endif
     int lc, lr;  // lane -> (column, row) inside the wave's C x R pixels
-    if (ACMMP_LANE_MAP == 1 && C == 8 && R == 8) {  // 16-lane groups of 4 x 4, row-major inside
-        lc = (l & 3) + 4 * ((l >> 4) & 1);
-        lr = ((l >> 2) & 3) + 4 * (l >> 5);
-    } else if (ACMMP_LANE_MAP == 2 && C == 8 && R == 8) {  // 16-lane groups of 4 x 4, column-major inside
+    if (ACMMP_LANE_MAP == 2 && C == 8 && R == 8) {
         lc = ((l >> 2) & 3) + 4 * ((l >> 4) & 1);
         lr = (l & 3) + 4 * (l >> 5);
-    } else if (ACMMP_LANE_MAP == 3 && C == 8 && R == 8) {  // 16-lane groups of 8 x 2, column-major inside
-        lc = (l >> 1) & 7;
-        lr = (l & 1) + 2 * (l >> 4);
     } else {
         lc = l % C;
         lr = l / C;
