@@ -98,6 +98,10 @@ int kv_upload(acmmp_ctx *ctx) {
         kv.pad[i] = ctx->pad_use[i];
         kv.ppitch[i] = ctx->pad_pitch[i];
         if (i > 0) kv.rel[i] = view_rel(ctx->cams[0], ctx->cams[i]);
+        {
+            const acmmp_camera &c = ctx->cams[i];
+            for (int k = 0; k < 3; ++k) kv.cw[i][k] = -(c.R[k] * c.t[0] + c.R[3 + k] * c.t[1] + c.R[6 + k] * c.t[2]);
+        }
         if (ctx->have_depths) {
             kv.dep[i] = ctx->dep[i];
             kv.dpitch[i] = ctx->dep_pitch[i];

@@ -53,6 +53,10 @@ struct KViews {
     //    (texel(c-1, r-1), texel(c-1, r)); a footprint is two records, 16 B.
     const float *pad[ACMMP_MAX_IMAGES];
     int ppitch[ACMMP_MAX_IMAGES];             // in records
+    // -(R^T t) of every camera, the world-frame offset Get3DPointonWorld_cu
+    // adds (src/ACMMP.cu:494-503), formed once on the host with the
+    // kernel's float expression (same operations, same order: exact)
+    float cw[ACMMP_MAX_IMAGES][3];
     const float *dep[ACMMP_MAX_IMAGES];       // pitched depth maps (geom consistency)
     int dpitch[ACMMP_MAX_IMAGES];
     int dw[ACMMP_MAX_IMAGES];

@@ -711,23 +711,36 @@ DEV float initial_cost(const KViews &kv, const float *tile, int tb, const PixPat
     return 2.0f;
 }
 
-DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
-    const float max_cost = 3.0f;
+// ComputeGeomConsistencyCost (src/ACMMP.cu:518-543), split so the view-
+// independent half is formed once per hypothesis: geom_ref is the world
+// point of the hypothesis at the pixel (ComputeDepthfromPlaneHypothesis +
+// Get3DPointonWorld_cu :480-504), geom_cost_at projects it into source v,
+// fetches the source depth and measures the reprojection error. Same
+// operations in the same order as the unsplit function (the camera offsets
+// -(R^T t) come precomputed in KViews::cw, formed by the same expression).
+struct GeomRef {
+    float Wp[3];
+};
+
+DEV GeomRef geom_ref(const KViews &kv, float4 h, int px, int py) {
     const acmmp_camera &rc = kv.cam[0];
-    const acmmp_camera &sc = kv.cam[v];
     const float depth = plane_depth(rc, h, px, py);
-    // Get3DPointonWorld_cu (:480-504)
     float X[3];
     X[0] = depth * ((float)px - rc.K[2]) / rc.K[0];
     X[1] = depth * ((float)py - rc.K[5]) / rc.K[4];
     X[2] = depth;
-    float Wp[3];
-    Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) +
-            -(rc.R[0] * rc.t[0] + rc.R[3] * rc.t[1] + rc.R[6] * rc.t[2]);
-    Wp[1] = (rc.R[1] * X[0] + rc.R[4] * X[1] + rc.R[7] * X[2]) +
-            -(rc.R[1] * rc.t[0] + rc.R[4] * rc.t[1] + rc.R[7] * rc.t[2]);
-    Wp[2] = (rc.R[2] * X[0] + rc.R[5] * X[1] + rc.R[8] * X[2]) +
-            -(rc.R[2] * rc.t[0] + rc.R[5] * rc.t[1] + rc.R[8] * rc.t[2]);
+    GeomRef g;
+    g.Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) + kv.cw[0][0];
+    g.Wp[1] = (rc.R[1] * X[0] + rc.R[4] * X[1] + rc.R[7] * X[2]) + kv.cw[0][1];
+    g.Wp[2] = (rc.R[2] * X[0] + rc.R[5] * X[1] + rc.R[8] * X[2]) + kv.cw[0][2];
+    return g;
+}
+
+DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py) {
+    const float max_cost = 3.0f;
+    const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
+    const float *Wp = g.Wp;
     // ProjectonCamera_cu (:506-516)
     float T[3];
     T[0] = sc.R[0] * Wp[0] + sc.R[1] * Wp[1] + sc.R[2] * Wp[2] + sc.t[0];
@@ -743,12 +756,9 @@ DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
     Y[1] = src_depth * (sy - sc.K[5]) / sc.K[4];
     Y[2] = src_depth;
     float Wq[3];
-    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) +
-            -(sc.R[0] * sc.t[0] + sc.R[3] * sc.t[1] + sc.R[6] * sc.t[2]);
-    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) +
-            -(sc.R[1] * sc.t[0] + sc.R[4] * sc.t[1] + sc.R[7] * sc.t[2]);
-    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) +
-            -(sc.R[2] * sc.t[0] + sc.R[5] * sc.t[1] + sc.R[8] * sc.t[2]);
+    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) + kv.cw[v][0];
+    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) + kv.cw[v][1];
+    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) + kv.cw[v][2];
     float U[3];
     U[0] = rc.R[0] * Wq[0] + rc.R[1] * Wq[1] + rc.R[2] * Wq[2] + rc.t[0];
     U[1] = rc.R[3] * Wq[0] + rc.R[4] * Wq[1] + rc.R[5] * Wq[2] + rc.t[1];
@@ -760,6 +770,10 @@ DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
     const float dr = (float)py - by;
     const float e = dm_sqrt(dc * dc + dr * dr);
     return (e < max_cost) ? e : max_cost;
+}
+
+DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
+    return geom_cost_at(kv, v, geom_ref(kv, h, px, py), px, py);
 }
 
 DEV dm_rng make_rng(const KViews &kv, int center, uint32_t phase) {
@@ -1370,14 +1384,14 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
         const bool fl = (flags >> i) & 1u;
-        float4 hi = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (prm.geom_consistency && fl) hi = cand(i);
+        GeomRef gi = {};
+        if (prm.geom_consistency && fl) gi = geom_ref(kv, cand(i), px, py);  // once per candidate
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
                 if (prm.geom_consistency) {
                     const float cij = cost_array[i][j];
-                    if (fl) fc += wj * (cij + 0.2f * geom_cost(kv, j + 1, hi, px, py));
+                    if (fl) fc += wj * (cij + 0.2f * geom_cost_at(kv, j + 1, gi, px, py));
                     else fc += wj * (cij + 0.1f * 3.0f);
                 } else {
                     fc += wj * cost_array[i][j];
@@ -1431,14 +1445,17 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         float tc = 0.0f;
         if (t >= 1) {
             tc = cmp_res(cand_lds, t - 1, pp.wo);
-        } else
+        } else {
+        GeomRef gnow = {};
+        if (prm.geom_consistency) gnow = geom_ref(kv, h, px, py);  // once for the current plane
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
                 const float c = bilateral_ncc<TX>(kv, tile, g.tb, pp, j + 1, px, py, h);
-                if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost(kv, j + 1, h, px, py));
+                if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost_at(kv, j + 1, gnow, px, py));
                 else tc += wj * c;
             }
+        }
         }
         tc /= weight_norm;
         if (t == 0) {
