@@ -304,6 +304,9 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
             "unit": "Ginst/s",
             "frac": round(pmc["td_busy_frac"], 4),
             "td_cycles_per_gather": round(pmc["td_cyc_per_inst"], 2),
+            "l1_accesses_per_gather": (round(pmc["tcp_accesses_per_gather"], 2)
+                                       if pmc.get("tcp_accesses_per_gather") == pmc.get("tcp_accesses_per_gather")
+                                       else None),
             "model": "achieved = TA_BUFFER_READ_WAVEFRONTS_sum per launch / launch_ms; peak = 256 CUs x clock "
                      "(GRBM_GUI_ACTIVE/8 / profiled duration) / (TD_TD_BUSY_sum / TA_BUFFER_READ_WAVEFRONTS_sum); "
                      "frac = TD_TD_BUSY_sum / (256 x GRBM_GUI_ACTIVE/8)",

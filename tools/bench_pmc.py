@@ -44,7 +44,7 @@ PASSES = [
     ("fetch", ["FETCH_SIZE", "GRBM_GUI_ACTIVE", "TD_TD_BUSY_sum", "TA_BUFFER_READ_WAVEFRONTS_sum",
                "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVES"]),
     ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_VALU",
-               "SQ_INSTS_VALU"]),
+               "SQ_INSTS_VALU", "TCP_TOTAL_CACHE_ACCESSES_sum", "TA_BUFFER_READ_WAVEFRONTS_sum"]),
 ]
 
 
@@ -132,6 +132,9 @@ def summarize(res: dict) -> dict:
         "lds_insts": mean(f, "SQ_INSTS_LDS"),
         "waves": mean(f, "SQ_WAVES"),
         "valu_insts": mean(w, "SQ_INSTS_VALU"),
+        # one TD cycle per L1 access (profiles/r04_td_addressing.md)
+        "tcp_accesses_per_gather": (mean(w, "TCP_TOTAL_CACHE_ACCESSES_sum") / mean(w, "TA_BUFFER_READ_WAVEFRONTS_sum")
+                                    if mean(w, "TA_BUFFER_READ_WAVEFRONTS_sum") > 0 else float("nan")),
         "valu_busy_frac": 4 * mean(w, "SQ_ACTIVE_INST_VALU") / ((mean(w, "GRBM_GUI_ACTIVE") / XCDS) * CUS * 4),
         "gpu_cycles_per_xcd": cyc_per_cu,
         "profiled_ms": statistics.mean(durs) if durs else float("nan"),
