@@ -320,7 +320,10 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // per k_sweep launch (profiles/r02_block_shape.md): 64 x 4 blocks of
 // 16 x 4 waves 4.66, 32 x 8 4.41, 16 x 16 4.28, 16 x 16 of 8 x 8 waves
 // 4.19, 8 x 32 4.18.
-constexpr int kBX = 16, kBY = 256 / kBX;
+#ifndef ACMMP_KBX
+#define ACMMP_KBX 16
+#endif
+constexpr int kBX = ACMMP_KBX, kBY = 256 / kBX;  // ACMMP_KBX: A/B builds only
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
 
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
