@@ -16,7 +16,8 @@ def _passes():
              "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7, "SQ_INSTS_VMEM_RD": 5.2e7, "SQ_INSTS_LDS": 4.7e7,
              "SQ_WAVES": 1.5e4}
     write = {"WRITE_SIZE": 3.0e5, "GRBM_GUI_ACTIVE": gui, "TA_TA_BUSY_sum": 1.28e9, "SQ_INSTS_VMEM_WR": 1.4e6,
-             "SQ_ACTIVE_INST_VALU": 1.92e9, "SQ_INSTS_VALU": 1.87e9}
+             "SQ_ACTIVE_INST_VALU": 1.92e9, "SQ_INSTS_VALU": 1.87e9, "TCP_TOTAL_CACHE_ACCESSES_sum": 1.8e9,
+             "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7}
     per = lambda d: {k: {0: v, 1: v} for k, v in d.items()}  # two dispatches
     return {"passes": {"fetch": {"counters": per(fetch), "durations_ms": [4.0, 4.0]},
                        "write": {"counters": per(write), "durations_ms": [4.0, 4.0]}}}
@@ -29,6 +30,7 @@ def test_summarize_fractions():
     assert abs(s["valu_busy_frac"] - 4 * 1.92e9 / (1e7 * 256 * 4)) < 1e-12
     assert s["hbm_bytes"] == (2 * 1.0e6 + 3.0e5) * 1024
     assert abs(s["clock_ghz"] - 2.5) < 1e-12
+    assert abs(s["tcp_accesses_per_gather"] - 36.0) < 1e-9
 
 
 def test_bench_roofline_block():
@@ -41,6 +43,7 @@ def test_bench_roofline_block():
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["traffic"] == s["hbm_bytes"]
     assert r["binding_unit"]["bound"] == "td-gather" and 0 < r["binding_unit"]["frac"] <= 1
+    assert r["binding_unit"]["l1_accesses_per_gather"] == 36.0
     assert r["valu"]["bound"] == "valu" and r["valu"]["frac"] == round(s["valu_busy_frac"], 4)
     assert r["hbm_physical"]["frac"] < 1
     for k in ("achieved", "peak", "unit", "frac", "traffic"):
