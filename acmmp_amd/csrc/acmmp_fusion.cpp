@@ -695,25 +695,13 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         auto bit = [](const uint64_t *w, size_t k) -> bool {
             return (__atomic_load_n(&w[k >> 6], __ATOMIC_RELAXED) >> (k & 63)) & 1ull;
         };
-        constexpr int kAhead = 6;  // pixels whose source mask words are prefetched (0, 6, 24: same, r03)
         constexpr uint32_t kSpMask = (1u << kSpBits) - 1;
         for (int r = 0; r < H; ++r) {
             const uint32_t *h = vh.hit[(size_t)r].data();
             const float *hx = vh.ex[(size_t)r].data();
             const uint16_t *nhr = vh.nhit[(size_t)r].data();
             const float *sumr = vh.sum[(size_t)r].data();
-            const uint32_t *hpf = h;
-            int cpf = 0;
-            auto prefetch_to = [&](int upto) {
-                for (; cpf < W && cpf < upto; ++cpf) {
-                    const int n = nhr[cpf];
-                    if (n == 0xffff) continue;
-                    for (int k = 0; k < n; ++k) __builtin_prefetch(&mw[hpf[k] >> kSpBits][(hpf[k] & kSpMask) >> 6]);
-                    hpf += n;
-                }
-            };
             for (int c = 0; c < W; ++c) {
-                prefetch_to(c + 1 + kAhead);
                 const size_t pc = (size_t)r * W + c;
                 const int nh = nhr[c];
                 if (nh == 0xffff) continue;
