@@ -43,13 +43,23 @@ constexpr int kTaps = 6;
 #define ACMMP_WAVE_ROWS 8
 #endif
 constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geom_of; A/B builds only)
+// Geometric-cost depth fetches issued ahead of their use (A/B builds only):
+// bit 0 the final candidate costs, bit 1 the current plane, bit 2 refinement.
+#ifndef ACMMP_GEOM_AHEAD
+#define ACMMP_GEOM_AHEAD 7
+#endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
 
 // ----------------------------------------------------------------- textures
+// Through the global address space: a generic (flat) load would also count
+// against lgkmcnt, so every later wait for a scalar or LDS load would drain
+// it too (the geometric cost's depth fetch could never overlap anything).
+typedef const __attribute__((address_space(1))) float gfloat;
+
 DEV float texel(const float *img, int pitch, int W, int H, int x, int y) {
     x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
     y = y < 0 ? 0 : (y > H - 1 ? H - 1 : y);
-    return img[y * pitch + x];
+    return ((gfloat *)img)[y * pitch + x];
 }
 
 // pin P2 (tex2D linear, clamp; src/ACMMP.cu:394)
@@ -739,9 +749,15 @@ DEV GeomRef geom_ref(const KViews &kv, float4 h, int px, int py) {
     return g;
 }
 
-DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py) {
-    const float max_cost = 3.0f;
-    const acmmp_camera &rc = kv.cam[0];
+// geom_cost_at in two halves, so a caller can issue the source-depth
+// fetches of several views (or one ahead of an NCC) before it consumes them:
+// geom_fetch projects into source v and loads the depth (always in bounds:
+// tex_trunc clamps, NaN included), geom_finish is the rest.
+struct GeomFetch {
+    float sx, sy, dep;
+};
+
+DEV GeomFetch geom_fetch(const KViews &kv, int v, const GeomRef &g) {
     const acmmp_camera &sc = kv.cam[v];
     const float *Wp = g.Wp;
     // ProjectonCamera_cu (:506-516)
@@ -750,9 +766,18 @@ DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py
     T[1] = sc.R[3] * Wp[0] + sc.R[4] * Wp[1] + sc.R[5] * Wp[2] + sc.t[1];
     T[2] = sc.R[6] * Wp[0] + sc.R[7] * Wp[1] + sc.R[8] * Wp[2] + sc.t[2];
     const float sd = sc.K[6] * T[0] + sc.K[7] * T[1] + sc.K[8] * T[2];
-    const float sx = (sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2]) / sd;
-    const float sy = (sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2]) / sd;
-    const float src_depth = tex_trunc(kv.dep[v], kv.dpitch[v], kv.dw[v], kv.dh[v], sx, sy);
+    GeomFetch f;
+    f.sx = (sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2]) / sd;
+    f.sy = (sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2]) / sd;
+    f.dep = tex_trunc(kv.dep[v], kv.dpitch[v], kv.dw[v], kv.dh[v], f.sx, f.sy);
+    return f;
+}
+
+DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int py) {
+    const float max_cost = 3.0f;
+    const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
+    const float sx = f.sx, sy = f.sy, src_depth = f.dep;
     if (src_depth == 0.0f) return max_cost;
     float Y[3];
     Y[0] = src_depth * (sx - sc.K[2]) / sc.K[0];
@@ -773,6 +798,10 @@ DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py
     const float dr = (float)py - by;
     const float e = dm_sqrt(dc * dc + dr * dr);
     return (e < max_cost) ? e : max_cost;
+}
+
+DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py) {
+    return geom_finish(kv, v, geom_fetch(kv, v, g), px, py);
 }
 
 DEV float geom_cost(const KViews &kv, int v, float4 h, int px, int py) {
@@ -1074,8 +1103,18 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
                 op.var = cmp_pd(lds, 2, otid);
                 op.inv_wsum = cmp_pd(lds, 3, otid);
                 const float4 h = lds[t * kThreads + otid];
-                const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, j + 1, og.px, og.py, h);
-                cmp_res(lds, t, otid) = kv.prm.geom_consistency ? cc + 0.2f * geom_cost(kv, j + 1, h, og.px, og.py) : cc;
+                if (ACMMP_GEOM_AHEAD & 4) {
+                    // the geometric depth fetch goes out ahead of the NCC's gathers
+                    GeomFetch gf = {};
+                    if (kv.prm.geom_consistency) gf = geom_fetch(kv, j + 1, geom_ref(kv, h, og.px, og.py));
+                    const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, j + 1, og.px, og.py, h);
+                    cmp_res(lds, t, otid) =
+                        kv.prm.geom_consistency ? cc + 0.2f * geom_finish(kv, j + 1, gf, og.px, og.py) : cc;
+                } else {
+                    const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, j + 1, og.px, og.py, h);
+                    cmp_res(lds, t, otid) =
+                        kv.prm.geom_consistency ? cc + 0.2f * geom_cost(kv, j + 1, h, og.px, og.py) : cc;
+                }
             }
         }
         wave_sync();
@@ -1383,6 +1422,42 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
                 }
             final_costs[i] = fc / weight_norm;
         }
+    } else if (ACMMP_GEOM_AHEAD & 1) {
+        // geometric: a flagged candidate's source-depth fetches for all views
+        // are issued before any is consumed (one memory latency per
+        // candidate, not one per view); the sum is the same ops in the same
+        // order, with unsampled views adding +0 as above (view 1 stands in
+        // for the padding views j >= nsrc, whose result is unused)
+        for (int i = 0; i < 8; ++i) {
+            float fc = 0.0f;
+            const bool fl = (flags >> i) & 1u;
+            // the candidate's cost row read whole and unconditionally (one
+            // batch of scratch loads, not one load and wait per sampled view)
+            float ci[NS];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) ci[j] = cost_array[i][j];
+            if (fl) {
+                const GeomRef gi = geom_ref(kv, cand(i), px, py);
+                GeomFetch gf[NS];
+#pragma unroll
+                for (int j = 0; j < NS; ++j) gf[j] = geom_fetch(kv, j < nsrc ? j + 1 : 1, gi);
+#pragma unroll
+                for (int j = 0; j < NS; ++j)
+                    if (j < nsrc) {
+                        const float wj = (float)vw.get(j);
+                        const float gc = geom_finish(kv, j + 1, gf[j], px, py);
+                        fc += wj > 0 ? wj * (ci[j] + 0.2f * gc) : 0.0f;
+                    }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NS; ++j)
+                    if (j < nsrc) {
+                        const float wj = (float)vw.get(j);
+                        fc += wj > 0 ? wj * (ci[j] + 0.1f * 3.0f) : 0.0f;
+                    }
+            }
+            final_costs[i] = fc / weight_norm;
+        }
     } else
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
@@ -1454,8 +1529,14 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         for (int j = 0; j < nsrc; ++j) {
             const float wj = (float)vw.get(j);
             if (wj > 0) {
+                // the geometric depth fetch goes out ahead of the NCC's gathers
+                GeomFetch gf = {};
+                if ((ACMMP_GEOM_AHEAD & 2) && prm.geom_consistency) gf = geom_fetch(kv, j + 1, gnow);
                 const float c = bilateral_ncc<TX>(kv, tile, g.tb, pp, j + 1, px, py, h);
-                if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost_at(kv, j + 1, gnow, px, py));
+                if (ACMMP_GEOM_AHEAD & 2) {
+                    if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_finish(kv, j + 1, gf, px, py));
+                    else tc += wj * c;
+                } else if (prm.geom_consistency) tc += wj * (c + 0.2f * geom_cost_at(kv, j + 1, gnow, px, py));
                 else tc += wj * c;
             }
         }
