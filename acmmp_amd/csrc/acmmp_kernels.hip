@@ -1171,146 +1171,104 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 
     // ---- adaptive checkerboard sampling (:813-991). cidx[d]: colour-split
     // index of direction d's winner; bit d of `same`: it is this colour.
+    // Each search reads all its costs first, unconditionally (a step outside
+    // the image reads the search's first, always valid, position instead),
+    // then runs the reference's comparison chain over them in the same order
+    // under the same conditions: one memory latency per search instead of
+    // one per step (a load inside a condition is issued and waited alone).
     int cidx[8];
     uint32_t flags = 0, same = 0;
-    float costMin;
-    if (py > 2) {  // up_far (opposite colour)
+    // far lines (opposite colour): 11 steps of 2 from distance 3;
+    // right_far's reversed comparison keeps the max (:879)
+    auto far_search = [&](auto valid, auto at, bool keep_max) -> int {
+        float c[11];
+#pragma unroll
+        for (int i = 0; i < 11; ++i) c[i] = cost_opp[at((i == 0 || valid(i)) ? i : 0)];
+        int b = 0;
+        float m = c[0];
+#pragma unroll
+        for (int i = 1; i < 11; ++i)
+            if (valid(i) && (keep_max ? (m < c[i]) : (c[i] < m))) { m = c[i]; b = i; }
+        return at(b);
+    };
+    if (py > 2) {  // up_far
         flags |= 1u << 1;
-        int by = py - 3;
-        costMin = cost_opp[CS(px, by)];
-        for (int i = 1; i < 11; ++i) {
-            if (py > 2 + 2 * i) {
-                const int ty = py - 3 - 2 * i;
-                const float c = cost_opp[CS(px, ty)];
-                if (c < costMin) { costMin = c; by = ty; }
-            }
-        }
-        cidx[1] = CS(px, by);
+        cidx[1] = far_search([&](int i) { return py > 2 + 2 * i; }, [&](int i) { return CS(px, py - 3 - 2 * i); }, false);
     }
     if (py < height - 3) {  // down_far
         flags |= 1u << 3;
-        int by = py + 3;
-        costMin = cost_opp[CS(px, by)];
-        for (int i = 1; i < 11; ++i) {
-            if (py < height - 3 - 2 * i) {
-                const int ty = py + 3 + 2 * i;
-                const float c = cost_opp[CS(px, ty)];
-                if (c < costMin) { costMin = c; by = ty; }
-            }
-        }
-        cidx[3] = CS(px, by);
+        cidx[3] = far_search([&](int i) { return py < height - 3 - 2 * i; },
+                             [&](int i) { return CS(px, py + 3 + 2 * i); }, false);
     }
     if (px > 2) {  // left_far
         flags |= 1u << 5;
-        int bx = px - 3;
-        costMin = cost_opp[CS(bx, py)];
-        for (int i = 1; i < 11; ++i) {
-            if (px > 2 + 2 * i) {
-                const int tx = px - 3 - 2 * i;
-                const float c = cost_opp[CS(tx, py)];
-                if (c < costMin) { costMin = c; bx = tx; }
-            }
-        }
-        cidx[5] = CS(bx, py);
+        cidx[5] = far_search([&](int i) { return px > 2 + 2 * i; }, [&](int i) { return CS(px - 3 - 2 * i, py); }, false);
     }
-    if (px < width - 3) {  // right_far: reversed comparison keeps the max (:879)
+    if (px < width - 3) {  // right_far
         flags |= 1u << 7;
-        int bx = px + 3;
-        costMin = cost_opp[CS(bx, py)];
-        for (int i = 1; i < 11; ++i) {
-            if (px < width - 3 - 2 * i) {
-                const int tx = px + 3 + 2 * i;
-                const float c = cost_opp[CS(tx, py)];
-                if (costMin < c) { costMin = c; bx = tx; }
-            }
-        }
-        cidx[7] = CS(bx, py);
+        cidx[7] = far_search([&](int i) { return px < width - 3 - 2 * i; },
+                             [&](int i) { return CS(px + 3 + 2 * i, py); }, true);
     }
     // near "V" searches: the base point is the opposite colour, the V arms
-    // are this colour (snapshot reads, pin A2).
+    // are this colour (snapshot reads, pin A2); arm k = 2 i + side is read
+    // from cost_same (own position `my` stands in for an arm off the image)
+    auto near_search = [&](int base, auto valid, auto at, int d) {
+        float c[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c[k] = cost_same[valid(k) ? at(k) : my];
+        int bi = base;
+        bool bs = false;
+        float m = cost_opp[base];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (valid(k) && c[k] < m) { m = c[k]; bi = at(k); bs = true; }
+        cidx[d] = bi;
+        same |= (uint32_t)bs << d;
+    };
     if (py > 0) {  // up_near
         flags |= 1u << 0;
-        int bi = CS(px, py - 1);
-        bool bs = false;
-        costMin = cost_opp[bi];
-        for (int i = 0; i < 3; ++i) {
-            const int ty = py - 2 - i;
-            if (py > 1 + i && px > i) {
-                const float c = cost_same[CS(px - i, ty)];
-                if (c < costMin) { costMin = c; bi = CS(px - i, ty); bs = true; }
-            }
-            if (py > 1 + i && px < width - 1 - i) {
-                const float c = cost_same[CS(px + i, ty)];
-                if (c < costMin) { costMin = c; bi = CS(px + i, ty); bs = true; }
-            }
-        }
-        cidx[0] = bi;
-        same |= (uint32_t)bs << 0;
+        near_search(CS(px, py - 1),
+                    [&](int k) { const int i = k >> 1; return py > 1 + i && ((k & 1) ? px < width - 1 - i : px > i); },
+                    [&](int k) { const int i = k >> 1; return CS((k & 1) ? px + i : px - i, py - 2 - i); }, 0);
     }
     if (py < height - 1) {  // down_near
         flags |= 1u << 2;
-        int bi = CS(px, py + 1);
-        bool bs = false;
-        costMin = cost_opp[bi];
-        for (int i = 0; i < 3; ++i) {
-            const int ty = py + 2 + i;
-            if (py < height - 2 - i && px > i) {
-                const float c = cost_same[CS(px - i, ty)];
-                if (c < costMin) { costMin = c; bi = CS(px - i, ty); bs = true; }
-            }
-            if (py < height - 2 - i && px < width - 1 - i) {
-                const float c = cost_same[CS(px + i, ty)];
-                if (c < costMin) { costMin = c; bi = CS(px + i, ty); bs = true; }
-            }
-        }
-        cidx[2] = bi;
-        same |= (uint32_t)bs << 2;
+        near_search(CS(px, py + 1),
+                    [&](int k) {
+                        const int i = k >> 1;
+                        return py < height - 2 - i && ((k & 1) ? px < width - 1 - i : px > i);
+                    },
+                    [&](int k) { const int i = k >> 1; return CS((k & 1) ? px + i : px - i, py + 2 + i); }, 2);
     }
     if (px > 0) {  // left_near
         flags |= 1u << 4;
-        int bi = CS(px - 1, py);
-        bool bs = false;
-        costMin = cost_opp[bi];
-        for (int i = 0; i < 3; ++i) {
-            const int tx = px - 2 - i;
-            if (px > 1 + i && py > i) {
-                const float c = cost_same[CS(tx, py - i)];
-                if (c < costMin) { costMin = c; bi = CS(tx, py - i); bs = true; }
-            }
-            if (px > 1 + i && py < height - 1 - i) {
-                const float c = cost_same[CS(tx, py + i)];
-                if (c < costMin) { costMin = c; bi = CS(tx, py + i); bs = true; }
-            }
-        }
-        cidx[4] = bi;
-        same |= (uint32_t)bs << 4;
+        near_search(CS(px - 1, py),
+                    [&](int k) { const int i = k >> 1; return px > 1 + i && ((k & 1) ? py < height - 1 - i : py > i); },
+                    [&](int k) { const int i = k >> 1; return CS(px - 2 - i, (k & 1) ? py + i : py - i); }, 4);
     }
     if (px < width - 1) {  // right_near
         flags |= 1u << 6;
-        int bi = CS(px + 1, py);
-        bool bs = false;
-        costMin = cost_opp[bi];
-        for (int i = 0; i < 3; ++i) {
-            const int tx = px + 2 + i;
-            if (px < width - 2 - i && py > i) {
-                const float c = cost_same[CS(tx, py - i)];
-                if (c < costMin) { costMin = c; bi = CS(tx, py - i); bs = true; }
-            }
-            if (px < width - 2 - i && py < height - 1 - i) {
-                const float c = cost_same[CS(tx, py + i)];
-                if (c < costMin) { costMin = c; bi = CS(tx, py + i); bs = true; }
-            }
-        }
-        cidx[6] = bi;
-        same |= (uint32_t)bs << 6;
+        near_search(CS(px + 1, py),
+                    [&](int k) {
+                        const int i = k >> 1;
+                        return px < width - 2 - i && ((k & 1) ? py < height - 1 - i : py > i);
+                    },
+                    [&](int k) { const int i = k >> 1; return CS(px + 2 + i, (k & 1) ? py + i : py - i); }, 6);
     }
 #undef CS
     // the 8 winners' planes, fetched once into this lane's LDS slots (the
     // NCC prologues then read them at LDS latency, not L2's)
     float4 *cand_slot = cand_lds + threadIdx.y * kBX + threadIdx.x;
+    // (all 8 loads issued together: an unflagged direction reads the own plane)
+    float4 cpl[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const bool f = (flags >> d) & 1u;
+        cpl[d] = ((f && !((same >> d) & 1u)) ? plane_opp : plane_same)[f ? cidx[d] : my];
+    }
 #pragma unroll
     for (int d = 0; d < 8; ++d)
-        if ((flags >> d) & 1u) cand_slot[d * kThreads] = (((same >> d) & 1u) ? plane_same : plane_opp)[cidx[d]];
+        if ((flags >> d) & 1u) cand_slot[d * kThreads] = cpl[d];
     auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
 
     PixPatch pp;
