@@ -339,14 +339,26 @@ constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
     const float *img = kv.img[0];
     const int pitch = kv.ipitch[0], W = kv.W, H = kv.H;
-    for (int e = threadIdx.y * kBX + threadIdx.x; e < kTileW * kTileH; e += kBX * kBY) {
+    // all of a thread's texels loaded before any is stored; a thread past the
+    // end repeats the last element (same value, same address), so no load
+    // sits in a conditional block waited on alone
+    constexpr int kN = kTileW * kTileH, kIt = (kN + kBX * kBY - 1) / (kBX * kBY);
+    float v[kIt];
+    int at[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        int e = threadIdx.y * kBX + threadIdx.x + it * kBX * kBY;
+        e = e < kN ? e : kN - 1;
         const int r = e / kTileW, kk = e - r * kTileW;
         const int yy = y0 - 5 + r;
         const int kc = k0 - 3 + kk;
         const int par = (yy + colour) & 1;
         const int xx = 2 * kc + par;
-        tile[e] = texel(img, pitch, W, H, xx, yy);
+        at[it] = e;
+        v[it] = texel(img, pitch, W, H, xx, yy);
     }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) tile[at[it]] = v[it];
 }
 
 // Reference-side invariants of ComputeBilateralNCC (src/ACMMP.cu:372-421):
@@ -1178,88 +1190,85 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     // one per step (a load inside a condition is issued and waited alone).
     int cidx[8];
     uint32_t flags = 0, same = 0;
-    // far lines (opposite colour): 11 steps of 2 from distance 3;
-    // right_far's reversed comparison keeps the max (:879)
-    auto far_search = [&](auto valid, auto at, bool keep_max) -> int {
-        float c[11];
-#pragma unroll
-        for (int i = 0; i < 11; ++i) c[i] = cost_opp[at((i == 0 || valid(i)) ? i : 0)];
-        int b = 0;
-        float m = c[0];
-#pragma unroll
-        for (int i = 1; i < 11; ++i)
-            if (valid(i) && (keep_max ? (m < c[i]) : (c[i] < m))) { m = c[i]; b = i; }
-        return at(b);
+    // Far lines d = 0..3 (up, down, left, right; bit 2d + 1): 11 steps of 2
+    // from distance 3 in the opposite colour; right_far's reversed comparison
+    // keeps the max (:879). Near "V"s d = 0..3 (bit 2d): the base point is
+    // the opposite colour, arm k = 2 i + side is this colour (snapshot reads,
+    // pin A2). A step off the image (or a direction that does not apply)
+    // reads a valid stand-in: CS(px, py) of the opposite colour, `my` of
+    // this one; its value is never compared.
+    auto far_valid = [&](int d, int i) -> bool {
+        return d == 0 ? py > 2 + 2 * i : d == 1 ? py < height - 3 - 2 * i : d == 2 ? px > 2 + 2 * i : px < width - 3 - 2 * i;
     };
-    if (py > 2) {  // up_far
-        flags |= 1u << 1;
-        cidx[1] = far_search([&](int i) { return py > 2 + 2 * i; }, [&](int i) { return CS(px, py - 3 - 2 * i); }, false);
-    }
-    if (py < height - 3) {  // down_far
-        flags |= 1u << 3;
-        cidx[3] = far_search([&](int i) { return py < height - 3 - 2 * i; },
-                             [&](int i) { return CS(px, py + 3 + 2 * i); }, false);
-    }
-    if (px > 2) {  // left_far
-        flags |= 1u << 5;
-        cidx[5] = far_search([&](int i) { return px > 2 + 2 * i; }, [&](int i) { return CS(px - 3 - 2 * i, py); }, false);
-    }
-    if (px < width - 3) {  // right_far
-        flags |= 1u << 7;
-        cidx[7] = far_search([&](int i) { return px < width - 3 - 2 * i; },
-                             [&](int i) { return CS(px + 3 + 2 * i, py); }, true);
-    }
-    // near "V" searches: the base point is the opposite colour, the V arms
-    // are this colour (snapshot reads, pin A2); arm k = 2 i + side is read
-    // from cost_same (own position `my` stands in for an arm off the image)
-    auto near_search = [&](int base, auto valid, auto at, int d) {
-        float c[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) c[k] = cost_same[valid(k) ? at(k) : my];
-        int bi = base;
-        bool bs = false;
-        float m = cost_opp[base];
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (valid(k) && c[k] < m) { m = c[k]; bi = at(k); bs = true; }
-        cidx[d] = bi;
-        same |= (uint32_t)bs << d;
+    auto far_at = [&](int d, int i) -> int {
+        return d == 0 ? CS(px, py - 3 - 2 * i)
+             : d == 1 ? CS(px, py + 3 + 2 * i)
+             : d == 2 ? CS(px - 3 - 2 * i, py)
+                      : CS(px + 3 + 2 * i, py);
     };
-    if (py > 0) {  // up_near
-        flags |= 1u << 0;
-        near_search(CS(px, py - 1),
-                    [&](int k) { const int i = k >> 1; return py > 1 + i && ((k & 1) ? px < width - 1 - i : px > i); },
-                    [&](int k) { const int i = k >> 1; return CS((k & 1) ? px + i : px - i, py - 2 - i); }, 0);
+    auto near_valid = [&](int d, int k) -> bool {
+        const int i = k >> 1, sd = k & 1;
+        return d == 0 ? py > 1 + i && (sd ? px < width - 1 - i : px > i)
+             : d == 1 ? py < height - 2 - i && (sd ? px < width - 1 - i : px > i)
+             : d == 2 ? px > 1 + i && (sd ? py < height - 1 - i : py > i)
+                      : px < width - 2 - i && (sd ? py < height - 1 - i : py > i);
+    };
+    auto near_at = [&](int d, int k) -> int {
+        const int i = k >> 1, sd = k & 1;
+        return d == 0 ? CS(sd ? px + i : px - i, py - 2 - i)
+             : d == 1 ? CS(sd ? px + i : px - i, py + 2 + i)
+             : d == 2 ? CS(px - 2 - i, sd ? py + i : py - i)
+                      : CS(px + 2 + i, sd ? py + i : py - i);
+    };
+    const bool near_on[4] = {py > 0, py < height - 1, px > 0, px < width - 1};
+    const int near_base[4] = {CS(px, py - 1), CS(px, py + 1), CS(px - 1, py), CS(px + 1, py)};
+    // every cost of the 8 searches is loaded before any comparison: one
+    // memory latency for all of them (a load inside a condition is issued
+    // and waited alone)
+    float cf[4][11], cn[4][6], cb[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+#pragma unroll
+        for (int i = 0; i < 11; ++i) cf[d][i] = cost_opp[far_valid(d, i) ? far_at(d, i) : CS(px, py)];
+        cb[d] = cost_opp[near_on[d] ? near_base[d] : CS(px, py)];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) cn[d][k] = cost_same[near_valid(d, k) ? near_at(d, k) : my];
     }
-    if (py < height - 1) {  // down_near
-        flags |= 1u << 2;
-        near_search(CS(px, py + 1),
-                    [&](int k) {
-                        const int i = k >> 1;
-                        return py < height - 2 - i && ((k & 1) ? px < width - 1 - i : px > i);
-                    },
-                    [&](int k) { const int i = k >> 1; return CS((k & 1) ? px + i : px - i, py + 2 + i); }, 2);
+    // the reference's comparison chains, same order, same conditions
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        if (far_valid(d, 0)) {
+            flags |= 1u << (2 * d + 1);
+            int b = 0;
+            float m = cf[d][0];
+#pragma unroll
+            for (int i = 1; i < 11; ++i)
+                if (far_valid(d, i) && (d == 3 ? (m < cf[d][i]) : (cf[d][i] < m))) { m = cf[d][i]; b = i; }
+            cidx[2 * d + 1] = far_at(d, b);
+        }
     }
-    if (px > 0) {  // left_near
-        flags |= 1u << 4;
-        near_search(CS(px - 1, py),
-                    [&](int k) { const int i = k >> 1; return px > 1 + i && ((k & 1) ? py < height - 1 - i : py > i); },
-                    [&](int k) { const int i = k >> 1; return CS(px - 2 - i, (k & 1) ? py + i : py - i); }, 4);
-    }
-    if (px < width - 1) {  // right_near
-        flags |= 1u << 6;
-        near_search(CS(px + 1, py),
-                    [&](int k) {
-                        const int i = k >> 1;
-                        return px < width - 2 - i && ((k & 1) ? py < height - 1 - i : py > i);
-                    },
-                    [&](int k) { const int i = k >> 1; return CS(px + 2 + i, (k & 1) ? py + i : py - i); }, 6);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        if (near_on[d]) {
+            flags |= 1u << (2 * d);
+            int bi = near_base[d];
+            bool bs = false;
+            float m = cb[d];
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (near_valid(d, k) && cn[d][k] < m) { m = cn[d][k]; bi = near_at(d, k); bs = true; }
+            cidx[2 * d] = bi;
+            same |= (uint32_t)bs << (2 * d);
+        }
     }
 #undef CS
     // the 8 winners' planes, fetched once into this lane's LDS slots (the
     // NCC prologues then read them at LDS latency, not L2's)
     float4 *cand_slot = cand_lds + threadIdx.y * kBX + threadIdx.x;
-    // (all 8 loads issued together: an unflagged direction reads the own plane)
+    // (all 8 loads issued together, and stored unconditionally so none is
+    // sunk into a conditional block and waited alone: an unflagged
+    // direction's slot gets the own plane, and every reader of a slot
+    // checks its flag first)
     float4 cpl[8];
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
@@ -1267,8 +1276,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         cpl[d] = ((f && !((same >> d) & 1u)) ? plane_opp : plane_same)[f ? cidx[d] : my];
     }
 #pragma unroll
-    for (int d = 0; d < 8; ++d)
-        if ((flags >> d) & 1u) cand_slot[d * kThreads] = cpl[d];
+    for (int d = 0; d < 8; ++d) cand_slot[d * kThreads] = cpl[d];
     auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
 
     PixPatch pp;
