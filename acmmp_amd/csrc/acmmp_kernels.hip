@@ -747,6 +747,20 @@ struct GeomRef {
     float Wp[3];
 };
 
+// -(R^T t) of camera v, component k. The product takes it from KViews::cw
+// (formed on the host by the same expression: bit-identical without
+// contraction); the fidelity-study build (ACMMP_CUDA_NUMERICS) forms it here
+// so the device's FMA contraction and FTZ apply to it as nvcc's --fmad does
+// to Get3DPointonWorld_cu (src/ACMMP.cu:490-504).
+DEV float cam_offset(const KViews &kv, int v, int k) {
+#ifdef ACMMP_CUDA_NUMERICS
+    const acmmp_camera &c = kv.cam[v];
+    return -(c.R[k] * c.t[0] + c.R[3 + k] * c.t[1] + c.R[6 + k] * c.t[2]);
+#else
+    return kv.cw[v][k];
+#endif
+}
+
 DEV GeomRef geom_ref(const KViews &kv, float4 h, int px, int py) {
     const acmmp_camera &rc = kv.cam[0];
     const float depth = plane_depth(rc, h, px, py);
@@ -755,9 +769,9 @@ DEV GeomRef geom_ref(const KViews &kv, float4 h, int px, int py) {
     X[1] = depth * ((float)py - rc.K[5]) / rc.K[4];
     X[2] = depth;
     GeomRef g;
-    g.Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) + kv.cw[0][0];
-    g.Wp[1] = (rc.R[1] * X[0] + rc.R[4] * X[1] + rc.R[7] * X[2]) + kv.cw[0][1];
-    g.Wp[2] = (rc.R[2] * X[0] + rc.R[5] * X[1] + rc.R[8] * X[2]) + kv.cw[0][2];
+    g.Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) + cam_offset(kv, 0, 0);
+    g.Wp[1] = (rc.R[1] * X[0] + rc.R[4] * X[1] + rc.R[7] * X[2]) + cam_offset(kv, 0, 1);
+    g.Wp[2] = (rc.R[2] * X[0] + rc.R[5] * X[1] + rc.R[8] * X[2]) + cam_offset(kv, 0, 2);
     return g;
 }
 
@@ -796,9 +810,9 @@ DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int p
     Y[1] = src_depth * (sy - sc.K[5]) / sc.K[4];
     Y[2] = src_depth;
     float Wq[3];
-    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) + kv.cw[v][0];
-    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) + kv.cw[v][1];
-    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) + kv.cw[v][2];
+    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) + cam_offset(kv, v, 0);
+    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) + cam_offset(kv, v, 1);
+    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) + cam_offset(kv, v, 2);
     float U[3];
     U[0] = rc.R[0] * Wq[0] + rc.R[1] * Wq[1] + rc.R[2] * Wq[2] + rc.t[0];
     U[1] = rc.R[3] * Wq[0] + rc.R[4] * Wq[1] + rc.R[5] * Wq[2] + rc.t[1];
@@ -1392,8 +1406,9 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         // geometric: a flagged candidate's source-depth fetches for all views
         // are issued before any is consumed (one memory latency per
         // candidate, not one per view); the sum is the same ops in the same
-        // order, with unsampled views adding +0 as above (view 1 stands in
-        // for the padding views j >= nsrc, whose result is unused)
+        // order, with unsampled views adding +0 as above. Only the nsrc real
+        // views are fetched and read (j < nsrc is wave-uniform, so the loads
+        // still go out together; padding slots j >= nsrc are never written)
         for (int i = 0; i < 8; ++i) {
             float fc = 0.0f;
             const bool fl = (flags >> i) & 1u;
@@ -1401,12 +1416,12 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             // batch of scratch loads, not one load and wait per sampled view)
             float ci[NS];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) ci[j] = cost_array[i][j];
+            for (int j = 0; j < NS; ++j) ci[j] = j < nsrc ? cost_array[i][j] : 0.0f;
             if (fl) {
                 const GeomRef gi = geom_ref(kv, cand(i), px, py);
                 GeomFetch gf[NS];
 #pragma unroll
-                for (int j = 0; j < NS; ++j) gf[j] = geom_fetch(kv, j < nsrc ? j + 1 : 1, gi);
+                for (int j = 0; j < NS; ++j) gf[j] = j < nsrc ? geom_fetch(kv, j + 1, gi) : GeomFetch{};
 #pragma unroll
                 for (int j = 0; j < NS; ++j)
                     if (j < nsrc) {
@@ -1923,9 +1938,19 @@ static int ns_bucket(int nsrc) {
     return 32;
 }
 
-#ifdef ACMMP_DEV_SUBSET  // resource/ISA inspection builds only: one instantiation (NS 9, u8 quads)
+#ifdef ACMMP_DEV_SUBSET  // resource/ISA inspection builds only: u8 quads, NS 9 (and 16/20/32 with ACMMP_DEV_ALL_NS)
 #define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
+#ifdef ACMMP_DEV_ALL_NS
+#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
+    switch (ns_bucket(h_kv.nsrc)) {                                                         \
+        case 9: KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;               \
+        case 16: KERNEL<16, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+        case 20: KERNEL<20, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+        default: KERNEL<32, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;             \
+    }
+#else
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
+#endif
 #else
 #define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...)                             \
     switch (ns_bucket(h_kv.nsrc)) {                                                         \

@@ -149,8 +149,14 @@ def main():
     geom_params.geom_consistency = 1
     work = list(enumerate(mine))
 
+    phase_s = {"photometric": 0.0, "exchange": 0.0, "geometric": 0.0}
+
     def step():
+        # every pass ends with its views' streams synchronised (EnginePool.finish),
+        # so the host clock between the phases times them without extra waits
+        t0 = time.perf_counter()
         rv.photometric_pass(photo_params)
+        t1 = time.perf_counter()
         if distributed:
             if backend == "nccl":  # RCCL over xGMI, device buffers
                 dist.all_gather_into_tensor(rv.all_depth, rv.my_depth)
@@ -161,11 +167,18 @@ def main():
             # the engines' streams do not wait on torch's/RCCL's: finish the
             # gather before a geometric view borrows all_depth
             torch.cuda.synchronize()
+        t2 = time.perf_counter()
         rv.geometric_pass(geom_params)
+        t3 = time.perf_counter()
+        phase_s["photometric"] += t1 - t0
+        phase_s["exchange"] += t2 - t1
+        phase_s["geometric"] += t3 - t2
 
     for _ in range(args.warmup):
         step()
     pool.reset_timing()
+    for k in phase_s:
+        phase_s[k] = 0.0
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -176,10 +189,15 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    mine_row = [elapsed, phase_s["photometric"], phase_s["exchange"], phase_s["geometric"], float(len(mine))]
+    rows = [mine_row]
     if distributed and world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        # every rank's own times (the headline takes the max of the walls)
+        tt = torch.tensor(mine_row, dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        gathered = [torch.empty_like(tt) for _ in range(world)]
+        dist.all_gather(gathered, tt)
+        rows = [[float(x) for x in g.cpu().tolist()] for g in gathered]
+        elapsed = max(r[0] for r in rows)
     timed_ms, timed_launches = pool.sweep_ms, pool.sweep_launches
     if args.pmc_child:
         pool.close()
@@ -236,6 +254,8 @@ def main():
                             f"geometric) = {value / 2:.2f} Mpix/s",
             "residency": "images, state and depth maps stay in HBM; results exported device-to-device "
                          "(no per-run D2H copy as in the reference's RunPatchMatch, src/ACMMP.cu:1453-1454)",
+            "ranks": rank_fields(rows, args.steps,
+                                 ("RCCL" if backend == "nccl" else "gloo") if distributed else None),
         },
         "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, streams),
     }
@@ -247,6 +267,29 @@ def main():
     pool.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def rank_fields(rows, steps, exchange):
+    """Per-rank attribution of the timed region: each row is
+    one rank's [wall s, photometric s, depth all-gather s, geometric s,
+    views], summed over the timed steps. Reports the spread of the pass
+    times over ranks, the all-gather's ms per step and each rank's view
+    count; the headline `value` is unchanged (max-over-ranks wall)."""
+    walls = [r[0] for r in rows]
+    passes = [r[1] + r[3] for r in rows]
+    gather_ms = [r[2] / steps * 1e3 for r in rows]
+    return {
+        "world": len(rows),
+        "views_per_rank": [int(r[4]) for r in rows],
+        "wall_s": {"min": round(min(walls), 4), "max": round(max(walls), 4)},
+        "pass_s_per_step": {"min": round(min(passes) / steps, 4), "max": round(max(passes) / steps, 4)},
+        "photometric_s_per_step": [round(r[1] / steps, 4) for r in rows],
+        "geometric_s_per_step": [round(r[3] / steps, 4) for r in rows],
+        "depth_allgather_ms_per_step": ({"min": round(min(gather_ms), 3), "max": round(max(gather_ms), 3),
+                                         "backend": exchange} if exchange else None),
+        "note": "host clock around each phase of every timed step on every rank (the passes end synchronised); "
+                "pass = photometric + geometric; the all-gather time includes waiting for the slowest rank",
+    }
 
 
 def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
@@ -270,6 +313,10 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "frac_is_algorithmic": True,
+        "frac_note": "algorithmic (L1-served) bytes over the HBM peak, not an HBM utilisation: see "
+                     "hbm_physical_frac (PMC bytes) and binding_unit / valu for what binds the kernel",
+        "hbm_physical_frac": None,
         "traffic": None,
         "algorithmic_bytes_per_launch": round(logical_bytes),
         "model": "SURVEY §8d / BASELINE.md §3: per pixel-iteration 14 (N-1) NCC x 724 B + 572 B state "
@@ -288,6 +335,7 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
     insts = pmc["gather_insts"]
     hbm_gbs = pmc["hbm_bytes"] / (iso_ms / 1e3) / 1e9
     out.update({
+        "hbm_physical_frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
         "traffic": round(pmc["hbm_bytes"]),
         "traffic_note": "(2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch, memory side of L2 (Infinity-Cache "
                         "hits included), FETCH doubled per the gfx950 calibration",
@@ -320,6 +368,18 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
         },
         "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
     })
+    if "l2_hit_rate" in pmc:
+        out["l2"] = {
+            "hit_rate": round(pmc["l2_hit_rate"], 4),
+            "l1_to_l2_reqs_per_gather": round(pmc["l1_to_l2_reqs_per_gather"], 3),
+            "memory_side_read_reqs": round(pmc["ea_read_reqs"]),
+            "memory_side_read_reqs_dram": round(pmc["ea_read_reqs_dram"]),
+            "read_bytes_calibrated": (round(pmc["read_bytes_calibrated"]) if "read_bytes_calibrated" in pmc
+                                      else None),
+            "note": "TCC_HIT/(HIT+MISS), TCP_TCC_READ_REQ per gather wave-instruction, TCC_EA0_RDREQ(_DRAM) per "
+                    "launch; read bytes = RDREQ x the bytes per request calibrated for dword gathers "
+                    "(tools/microbench/fetch_cal.hip)",
+        }
     return out
 
 

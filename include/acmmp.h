@@ -114,7 +114,8 @@ typedef struct acmmp_pass_options {
     int32_t planar_prior;
     int32_t hierarchy;
     int32_t multi_geometry;
-    int32_t seeded;             /* pSampler priors (src/acmmp_definitions.cpp:8-177): not supported */
+    int32_t seeded;             /* pSampler seeded plane priors (src/acmmp_definitions.cpp:8-177, :275-281):
+                                 * acmmp_prior_plane_estimate + SetPlanarPrior before the first RunPatchMatch */
     int32_t max_iterations;     /* <= 0: reference behaviour (2; SetGeomConsistencyParams forces 2) */
     uint32_t seed_lo;           /* Philox key of this pass */
     uint32_t seed_hi;

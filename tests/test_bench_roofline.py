@@ -18,9 +18,12 @@ def _passes():
     write = {"WRITE_SIZE": 3.0e5, "GRBM_GUI_ACTIVE": gui, "TA_TA_BUSY_sum": 1.28e9, "SQ_INSTS_VMEM_WR": 1.4e6,
              "SQ_ACTIVE_INST_VALU": 1.92e9, "SQ_INSTS_VALU": 1.87e9, "TCP_TOTAL_CACHE_ACCESSES_sum": 1.8e9,
              "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7}
+    l2 = {"TCC_HIT_sum": 3.0e8, "TCC_MISS_sum": 1.0e8, "TCC_EA0_RDREQ_sum": 2.0e7, "TCC_EA0_RDREQ_DRAM_sum": 1.5e7,
+          "TCP_TCC_READ_REQ_sum": 1.75e8, "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7, "GRBM_GUI_ACTIVE": gui}
     per = lambda d: {k: {0: v, 1: v} for k, v in d.items()}  # two dispatches
     return {"passes": {"fetch": {"counters": per(fetch), "durations_ms": [4.0, 4.0]},
-                       "write": {"counters": per(write), "durations_ms": [4.0, 4.0]}}}
+                       "write": {"counters": per(write), "durations_ms": [4.0, 4.0]},
+                       "l2": {"counters": per(l2), "durations_ms": [4.0, 4.0]}}}
 
 
 def test_summarize_fractions():
@@ -31,6 +34,9 @@ def test_summarize_fractions():
     assert s["hbm_bytes"] == (2 * 1.0e6 + 3.0e5) * 1024
     assert abs(s["clock_ghz"] - 2.5) < 1e-12
     assert abs(s["tcp_accesses_per_gather"] - 36.0) < 1e-9
+    assert abs(s["l2_hit_rate"] - 0.75) < 1e-12
+    assert abs(s["l1_to_l2_reqs_per_gather"] - 3.5) < 1e-12
+    assert s["ea_read_reqs"] == 2.0e7 and s["ea_read_reqs_dram"] == 1.5e7
 
 
 def test_bench_roofline_block():
@@ -48,3 +54,22 @@ def test_bench_roofline_block():
     assert r["hbm_physical"]["frac"] < 1
     for k in ("achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
+    # frac is over algorithmic bytes; the physical fraction sits beside it
+    assert r["frac_is_algorithmic"] is True
+    assert r["hbm_physical_frac"] == r["hbm_physical"]["frac"]
+    assert r["l2"]["hit_rate"] == 0.75 and r["l2"]["l1_to_l2_reqs_per_gather"] == 3.5
+
+
+def test_rank_fields():
+    """The N>1 attribution block: per-rank pass times, the
+    depth all-gather's ms per step and the view counts, from each rank's
+    [wall, photometric, all-gather, geometric, views] row summed over steps."""
+    import bench
+    rows = [[2.6, 1.2, 0.04, 1.3, 10.0], [2.7, 1.25, 0.02, 1.35, 10.0]]
+    f = bench.rank_fields(rows, 2, "RCCL")
+    assert f["world"] == 2 and f["views_per_rank"] == [10, 10]
+    assert f["wall_s"] == {"min": 2.6, "max": 2.7}
+    assert f["pass_s_per_step"] == {"min": 1.25, "max": 1.3}
+    assert f["depth_allgather_ms_per_step"]["min"] == 10.0 and f["depth_allgather_ms_per_step"]["max"] == 20.0
+    assert f["photometric_s_per_step"] == [0.6, 0.625]
+    assert bench.rank_fields(rows[:1], 2, None)["depth_allgather_ms_per_step"] is None

@@ -7,7 +7,12 @@ notice losing them:
   address space);
 - the checkerboard searches' costs are in flight together (a load inside a
   condition is sunk into its block and waited alone: one latency per step);
-- no resource regression: 2 waves/SIMD, at most 384 B/lane of scratch."""
+- no resource regression: 2 waves/SIMD for every source-count bucket (NS 9,
+  16, 20, 32), scratch no larger than round 5's per bucket.
+The search-cost check reads a scheduling depth (the deepest vmcnt wait), a
+property of this compiler's schedule, not of the source: it runs only under
+the hipcc it was tuned on (ROCm 7.2.0) and must be re-tuned on an upgrade.
+Resources and flat loads are checked under any hipcc."""
 import os
 import re
 import shutil
@@ -26,7 +31,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not ins
 def listing(tmp_path_factory):
     out = tmp_path_factory.mktemp("isa") / "dev_kernels.s"
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
-           "-fno-slp-vectorize", "-I../../include", "-DACMMP_DEV_SUBSET", "--cuda-device-only", "-S",
+           "-fno-slp-vectorize", "-I../../include", "-DACMMP_DEV_SUBSET", "-DACMMP_DEV_ALL_NS", "--cuda-device-only", "-S",
            "acmmp_kernels.hip", "-o", str(out), "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -43,7 +48,17 @@ def test_no_flat_loads_in_k_sweep(listing):
     assert not flat, flat[:5]
 
 
+TUNED_HIPCC = "roc-7.2.0"  # the compiler whose schedule the vmcnt threshold was read from
+
+
+def _hipcc_version():
+    r = subprocess.run([HIPCC, "--version"], capture_output=True, text=True, timeout=60)
+    return r.stdout + r.stderr
+
+
 def test_search_costs_in_flight_together(listing):
+    if TUNED_HIPCC not in _hipcc_version():
+        pytest.skip(f"vmcnt depth threshold tuned on {TUNED_HIPCC}; re-tune it for this hipcc")
     body, _ = listing
     # the 72 search costs are issued before the first comparison: the
     # deepest vmcnt wait of the kernel reaches the counter's limit (63)
@@ -51,9 +66,17 @@ def test_search_costs_in_flight_together(listing):
     assert max(depths) >= 60, max(depths)
 
 
-def test_resources(listing):
+# scratch per lane of each bucket at round 5 (cost_array[8][NS] dominates)
+SCRATCH_MAX = {9: 384, 16: 672, 20: 816, 32: 1264}
+
+
+@pytest.mark.parametrize("ns", sorted(SCRATCH_MAX))
+def test_resources(listing, ns):
     _, remarks = listing
-    sweep = remarks[remarks.index("k_sweep_f"):]
+    tag = f"Function Name: _ZN5acmmp9k_sweep_fILi{ns}ELi2EE"
+    assert tag in remarks, f"k_sweep_f<{ns}, u8> not instantiated"
+    sweep = remarks[remarks.index(tag):]
+    sweep = sweep[:sweep.index("Function Name:", len(tag))] if "Function Name:" in sweep[len(tag):] else sweep
     occ = int(re.search(r"Occupancy \[waves/SIMD\]: (\d+)", sweep).group(1))
     scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", sweep).group(1))
-    assert occ == 2 and scratch <= 384, (occ, scratch)
+    assert occ == 2 and scratch <= SCRATCH_MAX[ns], (ns, occ, scratch)

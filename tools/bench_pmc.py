@@ -45,7 +45,19 @@ PASSES = [
                "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVES"]),
     ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_VALU",
                "SQ_INSTS_VALU", "TCP_TOTAL_CACHE_ACCESSES_sum", "TA_BUFFER_READ_WAVEFRONTS_sum"]),
+    # L2 side: hit/miss, L1->L2 read requests, memory-side
+    # read requests (all, and those that went to DRAM rather than another
+    # die's cache), within the 4 TCC slots
+    ("l2", ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCP_TCC_READ_REQ_sum",
+            "TA_BUFFER_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]),
 ]
+
+# Bytes one memory-side read request (TCC_EA0_RDREQ) stands for in dword
+# gathers, calibrated by tools/microbench/fetch_cal.hip on a 2 GiB buffer
+# with a known count of touched 128-B lines (profiles/r05_fetch_cal.json).
+# None until calibrated: the read figure is then FETCH_SIZE x 2, the guide's
+# streaming correction.
+RDREQ_BYTES = None
 
 
 def _run(cmd, log, timeout):
@@ -105,6 +117,7 @@ def collect(bench_py: str, child_args: list, out_dir: str, timeout: float = 150.
 def summarize(res: dict) -> dict:
     f = res["passes"]["fetch"]["counters"]
     w = res["passes"]["write"]["counters"]
+    l2 = res["passes"].get("l2", {}).get("counters", {})
 
     def mean(m, name):
         vals = list(m.get(name, {}).values())
@@ -139,4 +152,26 @@ def summarize(res: dict) -> dict:
         "gpu_cycles_per_xcd": cyc_per_cu,
         "profiled_ms": statistics.mean(durs) if durs else float("nan"),
         "clock_ghz": cyc_per_cu / (statistics.mean(durs) * 1e6) if durs else float("nan"),
+        **l2_figures(l2, mean),
     }
+
+
+def l2_figures(l2: dict, mean) -> dict:
+    """Per-launch L2 figures of the 'l2' pass (empty when the pass is absent)."""
+    if not l2:
+        return {}
+    hit, miss = mean(l2, "TCC_HIT_sum"), mean(l2, "TCC_MISS_sum")
+    rdreq, dram = mean(l2, "TCC_EA0_RDREQ_sum"), mean(l2, "TCC_EA0_RDREQ_DRAM_sum")
+    gathers = mean(l2, "TA_BUFFER_READ_WAVEFRONTS_sum")
+    out = {
+        "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else float("nan"),
+        "l2_hits": hit,
+        "l2_misses": miss,
+        "l1_to_l2_read_reqs": mean(l2, "TCP_TCC_READ_REQ_sum"),
+        "l1_to_l2_reqs_per_gather": mean(l2, "TCP_TCC_READ_REQ_sum") / gathers if gathers > 0 else float("nan"),
+        "ea_read_reqs": rdreq,
+        "ea_read_reqs_dram": dram,
+    }
+    if RDREQ_BYTES:
+        out["read_bytes_calibrated"] = rdreq * RDREQ_BYTES
+    return out
