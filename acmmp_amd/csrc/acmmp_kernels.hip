@@ -1655,6 +1655,40 @@ __global__ __launch_bounds__(256, kSweepWaves) void k_sweep_f(const KViews *__re
     sweep_body<NS, TX>(kvp, st, colour, iter);
 }
 
+// T1 kernel: costs of a given plane per pixel against every source view
+// (same NCC code path as the sweep; blockIdx.z = colour).
+template <int NS, int TX>
+__global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
+                                                    float *out, float *out_init, uint32_t *out_views) {
+    __shared__ float tile[kTileW * kTileH];
+    __shared__ WSlot wlds[kSlots * kThreads];
+    const KViews &kv = *kvp;
+    const int colour = blockIdx.z;
+    const BlockXY blk = xcd_block();
+    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    __syncthreads();
+    const LaneGeom g = lane_geom(colour, blk);
+    if (g.px >= kv.W || g.py >= kv.H) return;
+    const int c = g.py * kv.W + g.px;
+    PixPatch pp;
+    pp.wo = threadIdx.y * kBX + threadIdx.x;
+    pp.w = wlds + pp.wo;
+    pp.rt = tile + g.tb;
+    pixel_patch(kv, tile, g.tb, g.s, pp);
+    const float4 h = planes[c];
+    if (out)
+        for (int v = 0; v < kv.nsrc; ++v)
+            out[(size_t)c * kv.nsrc + v] = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
+    if (out_init) {
+        uint32_t sel = 0;
+        out_init[c] = initial_cost<NS, TX>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
+        if (out_views) out_views[c] = sel;
+    }
+}
+
+#ifndef ACMMP_TX_UNIT
+// ---- non-templated kernels and every launcher: the main translation unit
+// only (the texel-form units below hold the templated instantiations)
 __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp, KState st) {
     const KViews &kv = *kvp;
     const int px = blockIdx.x * 64 + threadIdx.x;
@@ -1719,38 +1753,6 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
     }
     const int m = n / 2;
     ph[center].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
-}
-
-// T1 kernel: costs of a given plane per pixel against every source view.
-// T1 kernel: costs of a given plane per pixel against every source view
-// (same NCC code path as the sweep; blockIdx.z = colour).
-template <int NS, int TX>
-__global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
-                                                    float *out, float *out_init, uint32_t *out_views) {
-    __shared__ float tile[kTileW * kTileH];
-    __shared__ WSlot wlds[kSlots * kThreads];
-    const KViews &kv = *kvp;
-    const int colour = blockIdx.z;
-    const BlockXY blk = xcd_block();
-    load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
-    __syncthreads();
-    const LaneGeom g = lane_geom(colour, blk);
-    if (g.px >= kv.W || g.py >= kv.H) return;
-    const int c = g.py * kv.W + g.px;
-    PixPatch pp;
-    pp.wo = threadIdx.y * kBX + threadIdx.x;
-    pp.w = wlds + pp.wo;
-    pp.rt = tile + g.tb;
-    pixel_patch(kv, tile, g.tb, g.s, pp);
-    const float4 h = planes[c];
-    if (out)
-        for (int v = 0; v < kv.nsrc; ++v)
-            out[(size_t)c * kv.nsrc + v] = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, g.px, g.py, h);
-    if (out_init) {
-        uint32_t sel = 0;
-        out_init[c] = initial_cost<NS, TX>(kv, tile, g.tb, pp, g.px, g.py, h, sel);
-        if (out_views) out_views[c] = sel;
-    }
 }
 
 __global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kvp, const float4 *planes,
@@ -1929,6 +1931,8 @@ hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw
     return hipGetLastError();
 }
 
+#endif  // !ACMMP_TX_UNIT
+
 // Source-view count -> array capacity of the templated kernels.
 static int ns_bucket(int nsrc) {
     if (nsrc <= 4) return 4;
@@ -1939,7 +1943,6 @@ static int ns_bucket(int nsrc) {
 }
 
 #ifdef ACMMP_DEV_SUBSET  // resource/ISA inspection builds only: u8 quads, NS 9 (and 16/20/32 with ACMMP_DEV_ALL_NS)
-#define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
 #ifdef ACMMP_DEV_ALL_NS
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
     switch (ns_bucket(h_kv.nsrc)) {                                                         \
@@ -1951,33 +1954,78 @@ static int ns_bucket(int nsrc) {
 #else
 #define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...) KERNEL<9, 2><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__);
 #endif
+#define ACMMP_LAUNCH_INIT(GRID, STREAM, ...) ACMMP_LAUNCH_NS(k_init, GRID, dim3(kBX, kBY), STREAM, __VA_ARGS__)
+#define ACMMP_LAUNCH_SWEEP(GRID, STREAM, ...) ACMMP_LAUNCH_NS(k_sweep_f, GRID, dim3(kBX, kBY), STREAM, __VA_ARGS__)
+#define ACMMP_LAUNCH_EVAL(GRID, STREAM, ...) ACMMP_LAUNCH_NS(k_eval_costs, GRID, dim3(kBX, kBY), STREAM, __VA_ARGS__)
 #else
-#define ACMMP_LAUNCH_NSW(KERNEL, TX, GRID, BLOCK, STREAM, ...)                             \
-    switch (ns_bucket(h_kv.nsrc)) {                                                         \
-        case 4: KERNEL<4, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;              \
-        case 9: KERNEL<9, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;              \
-        case 16: KERNEL<16, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
-        case 20: KERNEL<20, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
-        default: KERNEL<32, TX><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__); break;            \
+// The templated kernels (k_init, k_sweep_f, k_eval_costs) are instantiated
+// per texel form in their own translation unit: acmmp_kernels.hip compiled
+// with -DACMMP_TX_UNIT=<form> (Makefile), 5 NS buckets each, so the build
+// compiles the 8 forms in parallel. These three functions per form are the
+// units' entry points; the main unit picks the form.
+template <int TX> hipError_t tx_launch_init(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s, KState st);
+template <int TX>
+hipError_t tx_launch_sweep(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s, KState st, int colour, int iter);
+template <int TX>
+hipError_t tx_launch_eval(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s, const float4 *planes, float *out,
+                          float *out_init, uint32_t *out_views);
+#define ACMMP_TX_FORMS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(8) X(10)
+#define ACMMP_TX_DECL(TX)                                                                                      \
+    template <> hipError_t tx_launch_init<TX>(const KViews *, int, dim3, hipStream_t, KState);                  \
+    template <> hipError_t tx_launch_sweep<TX>(const KViews *, int, dim3, hipStream_t, KState, int, int);       \
+    template <> hipError_t tx_launch_eval<TX>(const KViews *, int, dim3, hipStream_t, const float4 *, float *,  \
+                                              float *, uint32_t *);
+#ifdef ACMMP_TX_UNIT
+#define ACMMP_NS_SWITCH(KERNEL, GRID, STREAM, ...)                                                         \
+    switch (ns_bucket(nsrc)) {                                                                              \
+        case 4: KERNEL<4, ACMMP_TX_UNIT><<<GRID, dim3(kBX, kBY), 0, STREAM>>>(__VA_ARGS__); break;          \
+        case 9: KERNEL<9, ACMMP_TX_UNIT><<<GRID, dim3(kBX, kBY), 0, STREAM>>>(__VA_ARGS__); break;          \
+        case 16: KERNEL<16, ACMMP_TX_UNIT><<<GRID, dim3(kBX, kBY), 0, STREAM>>>(__VA_ARGS__); break;        \
+        case 20: KERNEL<20, ACMMP_TX_UNIT><<<GRID, dim3(kBX, kBY), 0, STREAM>>>(__VA_ARGS__); break;        \
+        default: KERNEL<32, ACMMP_TX_UNIT><<<GRID, dim3(kBX, kBY), 0, STREAM>>>(__VA_ARGS__); break;        \
     }
-
-// Source-view count -> array capacity; KViews::wide -> the integer record
-// index of views with 2^24 or more records; KViews::texel -> the texel form.
-#define ACMMP_LAUNCH_NS(KERNEL, GRID, BLOCK, STREAM, ...)                                  \
-    switch ((h_kv.wide ? kTxWide : 0) | (h_kv.texel == kTexelU8 ? kTxU8 : 0) |              \
-            (h_kv.texel == kTexelH16 ? kTxH16 : 0) | (h_kv.prm.texture_filter8 ? kTxFrac8 : 0)) { \
-        case 8: { ACMMP_LAUNCH_NSW(KERNEL, 8, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 10: { ACMMP_LAUNCH_NSW(KERNEL, 10, GRID, BLOCK, STREAM, __VA_ARGS__) } break;  \
-        case 0: { ACMMP_LAUNCH_NSW(KERNEL, 0, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 1: { ACMMP_LAUNCH_NSW(KERNEL, 1, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 2: { ACMMP_LAUNCH_NSW(KERNEL, 2, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 3: { ACMMP_LAUNCH_NSW(KERNEL, 3, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 4: { ACMMP_LAUNCH_NSW(KERNEL, 4, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        case 5: { ACMMP_LAUNCH_NSW(KERNEL, 5, GRID, BLOCK, STREAM, __VA_ARGS__) } break;    \
-        default: return hipErrorNotSupported; /* texture_filter8 with a wide or f16 form */ \
+template <>
+hipError_t tx_launch_init<ACMMP_TX_UNIT>(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s, KState st) {
+    ACMMP_NS_SWITCH(k_init, grid, s, d_kv, st);
+    return hipGetLastError();
+}
+template <>
+hipError_t tx_launch_sweep<ACMMP_TX_UNIT>(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s, KState st,
+                                          int colour, int iter) {
+    ACMMP_NS_SWITCH(k_sweep_f, grid, s, d_kv, st, colour, iter);
+    return hipGetLastError();
+}
+template <>
+hipError_t tx_launch_eval<ACMMP_TX_UNIT>(const KViews *d_kv, int nsrc, dim3 grid, hipStream_t s,
+                                         const float4 *planes, float *out, float *out_init, uint32_t *out_views) {
+    ACMMP_NS_SWITCH(k_eval_costs, grid, s, d_kv, planes, out, out_init, out_views);
+    return hipGetLastError();
+}
+#else
+ACMMP_TX_FORMS(ACMMP_TX_DECL)
+// KViews::wide -> the integer record index of views with 2^24 or more
+// records; KViews::texel -> the texel form; texture_filter8 -> 8-bit fractions
+static int tx_form(const KViews &h_kv) {
+    return (h_kv.wide ? kTxWide : 0) | (h_kv.texel == kTexelU8 ? kTxU8 : 0) |
+           (h_kv.texel == kTexelH16 ? kTxH16 : 0) | (h_kv.prm.texture_filter8 ? kTxFrac8 : 0);
+}
+#define ACMMP_TX_CASE(FN, TX, ...) case TX: return FN<TX>(__VA_ARGS__);
+#define ACMMP_TX_DISPATCH(FN, ...)                                                                   \
+    switch (tx_form(h_kv)) {                                                                          \
+        ACMMP_TX_CASE(FN, 0, __VA_ARGS__) ACMMP_TX_CASE(FN, 1, __VA_ARGS__) ACMMP_TX_CASE(FN, 2, __VA_ARGS__) \
+        ACMMP_TX_CASE(FN, 3, __VA_ARGS__) ACMMP_TX_CASE(FN, 4, __VA_ARGS__) ACMMP_TX_CASE(FN, 5, __VA_ARGS__) \
+        ACMMP_TX_CASE(FN, 8, __VA_ARGS__) ACMMP_TX_CASE(FN, 10, __VA_ARGS__)                          \
+        default: return hipErrorNotSupported; /* texture_filter8 with a wide or f16 form */           \
     }
+#define ACMMP_LAUNCH_INIT(GRID, STREAM, ...) ACMMP_TX_DISPATCH(tx_launch_init, d_kv, h_kv.nsrc, GRID, STREAM, st)
+#define ACMMP_LAUNCH_SWEEP(GRID, STREAM, ...) \
+    ACMMP_TX_DISPATCH(tx_launch_sweep, d_kv, h_kv.nsrc, GRID, STREAM, st, colour, iter)
+#define ACMMP_LAUNCH_EVAL(GRID, STREAM, ...) \
+    ACMMP_TX_DISPATCH(tx_launch_eval, d_kv, h_kv.nsrc, GRID, STREAM, planes, out, out_init, out_views)
+#endif
 #endif
 
+#ifndef ACMMP_TX_UNIT
 // Colour-split grid over image rows [st.y0, st.y1): whole blocks of kBY
 // rows from the block row holding y0 (the kernels skip rows outside).
 static dim3 cs_grid(const KViews &kv, const KState &st, int colours) {
@@ -1991,14 +2039,14 @@ static dim3 row_grid(int cols, const KState &st) {
 
 hipError_t launch_init(const KViews *d_kv, const KViews &h_kv, const KState &st, hipStream_t stream) {
     if (st.y1 <= st.y0) return hipSuccess;
-    ACMMP_LAUNCH_NS(k_init, cs_grid(h_kv, st, 2), dim3(kBX, kBY), stream, d_kv, st);
+    ACMMP_LAUNCH_INIT(cs_grid(h_kv, st, 2), stream, d_kv, st);
     return hipGetLastError();
 }
 
 hipError_t launch_sweep(const KViews *d_kv, const KViews &h_kv, const KState &st, int colour, int iter,
                         hipStream_t stream) {
     if (st.y1 <= st.y0) return hipSuccess;
-    ACMMP_LAUNCH_NS(k_sweep_f, cs_grid(h_kv, st, 1), dim3(kBX, kBY), stream, d_kv, st, colour, iter);
+    ACMMP_LAUNCH_SWEEP(cs_grid(h_kv, st, 1), stream, d_kv, st, colour, iter);
     return hipGetLastError();
 }
 
@@ -2019,8 +2067,7 @@ hipError_t launch_eval_costs(const KViews *d_kv, const KViews &h_kv, const float
                              float *out_init, uint32_t *out_views, hipStream_t stream) {
     KState all{};
     all.y1 = h_kv.H;
-    ACMMP_LAUNCH_NS(k_eval_costs, cs_grid(h_kv, all, 2), dim3(kBX, kBY), stream, d_kv, planes, out, out_init,
-                    out_views);
+    ACMMP_LAUNCH_EVAL(cs_grid(h_kv, all, 2), stream, d_kv, planes, out, out_init, out_views);
     return hipGetLastError();
 }
 
@@ -2030,5 +2077,6 @@ hipError_t launch_eval_geom(const KViews *d_kv, const KViews &h_kv, const float4
     k_eval_geom<<<grid, block, 0, stream>>>(d_kv, planes, out);
     return hipGetLastError();
 }
+#endif  // !ACMMP_TX_UNIT
 
 }  // namespace acmmp
