@@ -564,6 +564,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::vector<std::vector<float>> ex;        // their exp(-tmp_index)
         std::vector<std::vector<uint16_t>> nhit;   // hits per pixel; 0xffff = not live
         std::vector<std::vector<float>> sum;       // per pixel: sum of its hits' ex, ascending j
+        std::vector<std::vector<F3>> X;            // world point of each live pixel of row r, in order
     };
     for (size_t i = 0; i < n; ++i)
         if ((size_t)cols[i] * rows[i] > (size_t(1) << kSpBits) || problems[i].num_src_images > 32)
@@ -590,6 +591,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::vector<float> &hx = vh.ex[(size_t)r];
         std::vector<uint16_t> &nh = vh.nhit[(size_t)r];
         std::vector<float> &sum = vh.sum[(size_t)r];
+        std::vector<F3> &X = vh.X[(size_t)r];
         h.clear();
         hx.clear();
         nh.assign((size_t)W, 0xffff);
@@ -658,6 +660,9 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             nh[(size_t)rs.live[k]] = (uint16_t)(h.size() - k0);
             sum[(size_t)rs.live[k]] = total;
         }
+        // the walk emits an approved pixel's point from here (the same
+        // world_point call the reference makes at approval, :1012)
+        X.swap(rs.X);
     };
     std::vector<ViewHits> vhits(2);
     auto start_phase1 = [&](size_t i) {
@@ -666,6 +671,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         vh.ex.resize((size_t)rows[i]);
         vh.nhit.resize((size_t)rows[i]);
         vh.sum.resize((size_t)rows[i]);
+        vh.X.resize((size_t)rows[i]);
         return pool.submit(rows[i], [&, i](int r) { phase1(i, vhits[i & 1], r); });
     };
     std::vector<Point> cloud;
@@ -701,12 +707,14 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             const float *hx = vh.ex[(size_t)r].data();
             const uint16_t *nhr = vh.nhit[(size_t)r].data();
             const float *sumr = vh.sum[(size_t)r].data();
+            const F3 *xr = vh.X[(size_t)r].data();
             for (int c = 0; c < W; ++c) {
                 const size_t pc = (size_t)r * W + c;
                 const int nh = nhr[c];
                 if (nh == 0xffff) continue;
                 const uint32_t *hp = h;
                 const float *hxp = hx;
+                const F3 *xp = xr++;
                 h += nh;
                 hx += nh;
                 // masks[i] changes during view i only if i is its own source
@@ -733,11 +741,10 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                         if (!bit(mw[hp[k] >> kSpBits], hp[k] & kSpMask)) dynamic_consistency += hxp[k];
                 }
                 if (num_consistent >= con_num_thresh && (dynamic_consistency > consistency_scalar * num_consistent)) {
-                    const float ref_depth = depths[i][pc];
                     const float *ref_normal = &normals[i][pc * 3];
                     const uint8_t *bgr = &images[i][pc * 3];
                     Point p;
-                    p.coord = world_point(c, r, ref_depth, cameras[i]);
+                    p.coord = *xp;  // world_point(c, r, depths[i][pc], cameras[i]), formed in phase 1
                     p.normal = F3{ref_normal[0], ref_normal[1], ref_normal[2]};
                     p.color = F3{(float)bgr[0], (float)bgr[1], (float)bgr[2]};
                     cloud.push_back(p);

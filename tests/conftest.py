@@ -30,6 +30,41 @@ _FIRST = ["test_gpu_parity", "test_gpu_headline", "test_gpu_sweep_views", "test_
 _LAST = ["test_gpu_band", "test_gpu_distributed", "test_gpu_vp_cli", "test_gpu_cfg4"]
 
 
+# Multi-scale driver inputs shared by test_gpu_distributed.py and
+# test_gpu_vp_cli.py (same scenes, so the oracle pipeline — the slow part —
+# runs once per session; each driver writes its own output subfolder).
+def _ms_dense(tmp_path_factory, views):
+    from acmmp_amd import scene
+    d = str(tmp_path_factory.mktemp(f"dense_ms{views}"))
+    sc = scene.make_scene(num_views=views, width=1010, height=760)
+    scene.write_dense_folder(sc, d, num_src=2)
+    return d
+
+
+@pytest.fixture(scope="session")
+def ms4_dense(tmp_path_factory):
+    """4 views at 1010x760, 2 sources each: two scales of cfg4's schedule."""
+    return _ms_dense(tmp_path_factory, 4)
+
+
+@pytest.fixture(scope="session")
+def ms3_dense(tmp_path_factory):
+    """3 views at 1010x760: at world 2 the third is split in row bands."""
+    return _ms_dense(tmp_path_factory, 3)
+
+
+@pytest.fixture(scope="session")
+def ms4_oracle_maps(ms4_dense):
+    from oracle_pipeline import OraclePipeline
+    return OraclePipeline(ms4_dense).run_multi_scale("jacobi")
+
+
+@pytest.fixture(scope="session")
+def ms3_oracle_maps(ms3_dense):
+    from oracle_pipeline import OraclePipeline
+    return OraclePipeline(ms3_dense).run_multi_scale("jacobi")
+
+
 def _file_rank(item):
     name = os.path.splitext(os.path.basename(str(item.fspath)))[0]
     if name in _FIRST:

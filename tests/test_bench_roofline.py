@@ -18,7 +18,7 @@ def _passes():
     write = {"WRITE_SIZE": 3.0e5, "GRBM_GUI_ACTIVE": gui, "TA_TA_BUSY_sum": 1.28e9, "SQ_INSTS_VMEM_WR": 1.4e6,
              "SQ_ACTIVE_INST_VALU": 1.92e9, "SQ_INSTS_VALU": 1.87e9, "TCP_TOTAL_CACHE_ACCESSES_sum": 1.8e9,
              "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7}
-    l2 = {"TCC_HIT_sum": 3.0e8, "TCC_MISS_sum": 1.0e8, "TCC_EA0_RDREQ_sum": 2.0e7, "TCC_EA0_RDREQ_DRAM_sum": 1.5e7,
+    l2 = {"TCC_HIT_sum": 3.0e8, "TCC_MISS_sum": 1.0e8, "TCC_EA0_RDREQ_sum": 2.0e7, "TCC_EA0_RDREQ_128B_sum": 1.5e7,
           "TCP_TCC_READ_REQ_sum": 1.75e8, "TA_BUFFER_READ_WAVEFRONTS_sum": 5.0e7, "GRBM_GUI_ACTIVE": gui}
     per = lambda d: {k: {0: v, 1: v} for k, v in d.items()}  # two dispatches
     return {"passes": {"fetch": {"counters": per(fetch), "durations_ms": [4.0, 4.0]},
@@ -36,7 +36,8 @@ def test_summarize_fractions():
     assert abs(s["tcp_accesses_per_gather"] - 36.0) < 1e-9
     assert abs(s["l2_hit_rate"] - 0.75) < 1e-12
     assert abs(s["l1_to_l2_reqs_per_gather"] - 3.5) < 1e-12
-    assert s["ea_read_reqs"] == 2.0e7 and s["ea_read_reqs_dram"] == 1.5e7
+    assert s["ea_read_reqs"] == 2.0e7 and s["ea_read_reqs_128b"] == 1.5e7
+    assert s["read_bytes_calibrated"] == 128 * 1.5e7 + 64 * 0.5e7
 
 
 def test_bench_roofline_block():

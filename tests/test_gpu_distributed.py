@@ -103,34 +103,28 @@ def test_world1_nccl_process_group_matches_oracle_jacobi(dense, jacobi_maps):
 
 
 @pytest.mark.timeout(600)
-def test_world2_multi_scale_matches_oracle_jacobi(tmp_path):
+def test_world2_multi_scale_matches_oracle_jacobi(ms4_dense, ms4_oracle_maps):
     """cfg4's schedule (src/main_ACMMP.cpp:96-176) view-parallel: two scales
     (1010x760 -> 505x380 first), photometric + planar, two geometric passes,
     JBU, hierarchy + planar, two geometric passes — two ranks on the one GPU
     against the oracle pipeline in Jacobi order, every .dmb bit-exact."""
-    d = str(tmp_path / "dense_ms")
-    sc = scene.make_scene(num_views=4, width=1010, height=760)
-    scene.write_dense_folder(sc, d, num_src=2)
+    d = ms4_dense
     got = _spawn(2, d, "gloo", "/VPMS")
     assert sorted(got[0][0] + got[1][0]) == list(range(4)) and got[0][0] and got[1][0]
-    maps = OraclePipeline(d).run_multi_scale("jacobi")
-    assert _compare(d + "/VPMS", maps) == 4 * 4
+    assert _compare(d + "/VPMS", ms4_oracle_maps) == 4 * 4
 
 
 @pytest.mark.timeout(600)
-def test_world2_multi_scale_split_tail_matches_oracle_jacobi(tmp_path):
+def test_world2_multi_scale_split_tail_matches_oracle_jacobi(ms3_dense, ms3_oracle_maps):
     """The same schedule with 3 views on 2 ranks: the third view is split in
     row bands over both ranks in every pass — photometric + planar prior
     (prior built on both ranks from the gathered first run), geometric,
     JBU + hierarchy — and every .dmb stays bit-exact to the oracle."""
-    d = str(tmp_path / "dense_ms3")
-    sc = scene.make_scene(num_views=3, width=1010, height=760)
-    scene.write_dense_folder(sc, d, num_src=2)
+    d = ms3_dense
     got = _spawn(2, d, "gloo", "/VPMS3")
     assert got[0][1] == got[1][1] == [2]
     assert sorted(got[0][0] + got[1][0]) == [0, 1, 2]
-    maps = OraclePipeline(d).run_multi_scale("jacobi")
-    assert _compare(d + "/VPMS3", maps) == 3 * 4
+    assert _compare(d + "/VPMS3", ms3_oracle_maps) == 3 * 4
 
 
 def test_bench_under_torchrun_nccl_world1():

@@ -78,28 +78,22 @@ def test_world2_tcp_matches_oracle_jacobi_and_fuses(dense, jacobi_maps, split):
 
 
 @pytest.mark.timeout(900)
-def test_world2_tcp_multi_scale_matches_oracle_jacobi(tmp_path):
+def test_world2_tcp_multi_scale_matches_oracle_jacobi(ms4_dense, ms4_oracle_maps):
     """Two scales (1010x760 -> 505x380 first): planar pass, two geometric
     passes, JBU + hierarchy + planar, two geometric passes."""
-    d = str(tmp_path / "dense_ms")
-    sc = scene.make_scene(num_views=4, width=1010, height=760)
-    scene.write_dense_folder(sc, d, num_src=2)
+    d = ms4_dense
     _launch(d, "/CVPMS", 2, "tcp", ["--no_fusion"], timeout=600)
-    maps = OraclePipeline(d).run_multi_scale("jacobi")
-    assert _compare(d + "/CVPMS", maps) == 4 * 4
+    assert _compare(d + "/CVPMS", ms4_oracle_maps) == 4 * 4
 
 
 @pytest.mark.timeout(900)
-def test_world2_tcp_multi_scale_split_tail_matches_oracle_jacobi(tmp_path):
+def test_world2_tcp_multi_scale_split_tail_matches_oracle_jacobi(ms3_dense, ms3_oracle_maps):
     """3 views on 2 ranks through the multi-scale schedule: the third view in
     two row bands in every pass (planar prior rebuilt on both ranks, JBU and
     hierarchy inputs on both), every .dmb bit-exact."""
-    d = str(tmp_path / "dense_ms3")
-    sc = scene.make_scene(num_views=3, width=1010, height=760)
-    scene.write_dense_folder(sc, d, num_src=2)
+    d = ms3_dense
     _launch(d, "/CVPMS3", 2, "tcp", ["--no_fusion"], timeout=600)
-    maps = OraclePipeline(d).run_multi_scale("jacobi")
-    assert _compare(d + "/CVPMS3", maps) == 3 * 4
+    assert _compare(d + "/CVPMS3", ms3_oracle_maps) == 3 * 4
 
 
 @pytest.mark.timeout(900)

@@ -46,18 +46,20 @@ PASSES = [
     ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_VALU",
                "SQ_INSTS_VALU", "TCP_TOTAL_CACHE_ACCESSES_sum", "TA_BUFFER_READ_WAVEFRONTS_sum"]),
     # L2 side: hit/miss, L1->L2 read requests, memory-side
-    # read requests (all, and those that went to DRAM rather than another
-    # die's cache), within the 4 TCC slots
-    ("l2", ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCP_TCC_READ_REQ_sum",
+    # read requests (all, and the 128-B ones), within the 4 TCC slots
+    ("l2", ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_128B_sum", "TCP_TCC_READ_REQ_sum",
             "TA_BUFFER_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]),
 ]
 
-# Bytes one memory-side read request (TCC_EA0_RDREQ) stands for in dword
-# gathers, calibrated by tools/microbench/fetch_cal.hip on a 2 GiB buffer
-# with a known count of touched 128-B lines (profiles/r05_fetch_cal.json).
-# None until calibrated: the read figure is then FETCH_SIZE x 2, the guide's
-# streaming correction.
-RDREQ_BYTES = None
+# Memory-side read bytes, calibrated for dword gathers by
+# tools/microbench/fetch_cal.hip (profiles/r05_fetch_cal.json): a 2 GiB
+# buffer read with dwordx4 streams, dword streams and one dword per 128-B
+# line, 64-B half line, 32-B sector or random line gives exactly one
+# TCC_EA0_RDREQ_128B per touched 128-B line in every pattern, and FETCH_SIZE
+# = 64 B per line: FETCH_SIZE tallies a 128-B request as 64 B whatever the
+# access width. So read bytes = 128 x RDREQ_128B + 64 x the other requests
+# (32-B requests are counted as 64 here: an upper bound; the fetch pass's
+# FETCH_SIZE x 2 is the same figure when every request is 128 B).
 
 
 def _run(cmd, log, timeout):
@@ -161,7 +163,7 @@ def l2_figures(l2: dict, mean) -> dict:
     if not l2:
         return {}
     hit, miss = mean(l2, "TCC_HIT_sum"), mean(l2, "TCC_MISS_sum")
-    rdreq, dram = mean(l2, "TCC_EA0_RDREQ_sum"), mean(l2, "TCC_EA0_RDREQ_DRAM_sum")
+    rdreq, r128 = mean(l2, "TCC_EA0_RDREQ_sum"), mean(l2, "TCC_EA0_RDREQ_128B_sum")
     gathers = mean(l2, "TA_BUFFER_READ_WAVEFRONTS_sum")
     out = {
         "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else float("nan"),
@@ -170,8 +172,7 @@ def l2_figures(l2: dict, mean) -> dict:
         "l1_to_l2_read_reqs": mean(l2, "TCP_TCC_READ_REQ_sum"),
         "l1_to_l2_reqs_per_gather": mean(l2, "TCP_TCC_READ_REQ_sum") / gathers if gathers > 0 else float("nan"),
         "ea_read_reqs": rdreq,
-        "ea_read_reqs_dram": dram,
+        "ea_read_reqs_128b": r128,
+        "read_bytes_calibrated": 128.0 * r128 + 64.0 * (rdreq - r128),
     }
-    if RDREQ_BYTES:
-        out["read_bytes_calibrated"] = rdreq * RDREQ_BYTES
     return out

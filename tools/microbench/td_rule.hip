@@ -11,7 +11,9 @@
 __device__ unsigned sbl32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
 
-constexpr int ITERS = 64, UNROLL = 8, NPAT = 12;
+constexpr int ITERS = 64, UNROLL = 8, NPAT = 16;
+
+__device__ constexpr int kShare[8] = {0, 0, 2, 4, 6, 6, 8, 10};
 
 // record (dword) of lane i; patterns documented in kName
 __device__ int lane_record(int pat, int i) {
@@ -27,7 +29,14 @@ __device__ int lane_record(int pat, int i) {
         case 8: return (i & 7) * 2 + (i >> 3) * 16;       // 8 lanes per line (stride 8 B): 8 lines
         case 9: return (i & 15) + (i >> 4) * 16 * 8;      // 16 lanes per line, lines 512 B apart: 4 lines
         case 10: return (i & 1) + (i >> 1) * 4;           // lane pairs on adjacent dwords, pairs 16 B apart
-        default: return (i & 31) * 16 + (i >> 5);         // lanes i, i+32 share a line: 32 lines
+        case 11: return (i & 31) * 16 + (i >> 5);         // lanes i, i+32 share a line: 32 lines
+        // (round 5) the 8 lanes of each (quarter, parity) group on ONE pixel's
+        // patch row (the shared-plane bound of DESIGN.md §5): dwords
+        // {0,0,2,4,6,6,8,10} of a 512-B-apart window per group
+        case 12: return ((i >> 4) * 2 + (i & 1)) * 128 + kShare[(i >> 1) & 7];       // span 0..40 B: one line
+        case 13: return ((i >> 4) * 2 + (i & 1)) * 128 + 10 + kShare[(i >> 1) & 7];  // 40..84 B: two lines
+        case 14: return ((i >> 4) * 2 + (i & 1)) * 128;                               // group on one dword
+        default: return ((i >> 4) * 2 + (i & 1)) * 128 + ((i >> 1) & 7);             // group on 8 consecutive dwords
     }
 }
 
