@@ -1695,6 +1695,10 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             final_costs[i] = fc / weight_norm;
         }
     } else if (ACMMP_GEOM_AHEAD & 1) {
+        // views sampled by some lane of the wave (bit j; nsrc <= 32, so
+        // padding slots j >= nsrc never appear)
+        uint32_t wave_views = 0;
+        for (int j = 0; j < nsrc; ++j) wave_views |= (__ballot(vw.get(j) > 0) != 0 ? 1u : 0u) << j;
         // geometric: a flagged candidate's source-depth fetches for all views
         // are issued before any is consumed (one memory latency per
         // candidate, not one per view); the sum is the same ops in the same
@@ -1710,13 +1714,16 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 #pragma unroll
             for (int j = 0; j < NS; ++j) ci[j] = j < nsrc ? cost_array[i][j] : 0.0f;
             if (fl) {
+                // views no lane of the wave sampled add +0 for every lane:
+                // their geometric cost is not finished (wave-uniform skip;
+                // the fetches stay unconditional, one batch per candidate)
                 const GeomRef gi = geom_ref(kv, cand(i), px, py);
                 GeomFetch gf[NS];
 #pragma unroll
                 for (int j = 0; j < NS; ++j) gf[j] = j < nsrc ? geom_fetch(kv, j + 1, gi) : GeomFetch{};
 #pragma unroll
                 for (int j = 0; j < NS; ++j)
-                    if (j < nsrc) {
+                    if ((wave_views >> j) & 1u) {
                         const float wj = (float)vw.get(j);
                         const float gc = geom_finish(kv, j + 1, gf[j], px, py);
                         fc += wj > 0 ? wj * (ci[j] + 0.2f * gc) : 0.0f;

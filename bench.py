@@ -373,12 +373,11 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
             "hit_rate": round(pmc["l2_hit_rate"], 4),
             "l1_to_l2_reqs_per_gather": round(pmc["l1_to_l2_reqs_per_gather"], 3),
             "memory_side_read_reqs": round(pmc["ea_read_reqs"]),
-            "memory_side_read_reqs_dram": round(pmc["ea_read_reqs_dram"]),
-            "read_bytes_calibrated": (round(pmc["read_bytes_calibrated"]) if "read_bytes_calibrated" in pmc
-                                      else None),
-            "note": "TCC_HIT/(HIT+MISS), TCP_TCC_READ_REQ per gather wave-instruction, TCC_EA0_RDREQ(_DRAM) per "
-                    "launch; read bytes = RDREQ x the bytes per request calibrated for dword gathers "
-                    "(tools/microbench/fetch_cal.hip)",
+            "memory_side_read_reqs_128b": round(pmc["ea_read_reqs_128b"]),
+            "read_bytes_calibrated": round(pmc["read_bytes_calibrated"]),
+            "note": "TCC_HIT/(HIT+MISS), TCP_TCC_READ_REQ per gather wave-instruction, TCC_EA0_RDREQ(_128B) per "
+                    "launch; read bytes = 128 x RDREQ_128B + 64 x the other requests, calibrated for dword gathers "
+                    "(tools/microbench/fetch_cal.hip, profiles/r05_fetch_cal.json)",
         }
     return out
 
