@@ -126,12 +126,6 @@ int kv_upload(acmmp_ctx *ctx) {
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
     kv.texel = ctx->pad_texel;
-    // Phase A pipelined from iteration 1 of a photometric pass and from the
-    // first of a geometric one (profiles/r05_launch_profile.jsonl);
-    // ACMMP_PIPE_FROM="p,g" overrides (A/B runs; a large value disables it)
-    kv.pipe_from[0] = 1;
-    kv.pipe_from[1] = 0;
-    if (const char *e = std::getenv("ACMMP_PIPE_FROM")) std::sscanf(e, "%d,%d", &kv.pipe_from[0], &kv.pipe_from[1]);
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737

@@ -66,10 +66,6 @@ struct KViews {
     int texel;                                // form of pad[]: kTexelF32 / kTexelU8 / kTexelH16
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
-    // first iteration whose Phase A runs as one NCC pipeline (ncc_stream), for
-    // photometric [0] and geometric [1] passes: random planes (iteration 0 of
-    // a photometric pass) thrash L1 when consecutive calls overlap
-    int pipe_from[2];
 };
 
 struct KState {

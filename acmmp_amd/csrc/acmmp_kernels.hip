@@ -49,19 +49,6 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
-// Phase A's NCC calls as one software pipeline (ncc_stream); 0 = one call at
-// a time (A/B builds only)
-#ifndef ACMMP_PIPE
-#define ACMMP_PIPE 1
-#endif
-// timing-only builds: Phase A alone (sweep_body)
-#ifndef ACMMP_PHASE_A_ONLY
-#define ACMMP_PHASE_A_ONLY 0
-#endif
-// timing-only bound builds (ncc_prep): lanes per shared pixel plane, 1 = off
-#ifndef ACMMP_UB_SHARE
-#define ACMMP_UB_SHARE 1
-#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -487,17 +474,17 @@ struct RowFetch {
 // Projection, clamp, fractions and record index of patch row jj, and its 6
 // loads issued (not waited for).
 template <bool FAST, int TX>
-DEV void fetch_row(const SrcImage &im, f2v h1, f2v h4, f2v h7, const f2v *cx, const f2v *cy, const f2v *cz,
-                   int py, int jj, RowFetch<TX> &rf) {
+DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
+                   RowFetch<TX> &rf) {
     constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
     constexpr bool F8 = (TX & kTxFrac8) != 0;
     const f2v fw = splat((float)im.W), fh = splat((float)im.H);
     const f2v y = splat((float)(py - 5 + 2 * jj));
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-        const f2v hx = fma2(h1, y, cx[p]);
-        const f2v hy = fma2(h4, y, cy[p]);
-        const f2v hz = fma2(h7, y, cz[p]);
+        const f2v hx = fma2(splat(H[1]), y, cx[p]);
+        const f2v hy = fma2(splat(H[4]), y, cy[p]);
+        const f2v hz = fma2(splat(H[7]), y, cz[p]);
         f2v inv;
         if (FAST) {  // v_rcp + one Newton step == IEEE 1/z in the window
             const f2v r = f2v{__builtin_amdgcn_rcpf(hz.x), __builtin_amdgcn_rcpf(hz.y)};
@@ -638,12 +625,12 @@ DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, cons
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
     // two rows per trip (ping-pong fetch buffers, no register copies)
     RowFetch<TX> ra, rb;
-    fetch_row<FAST, TX>(im, splat(H[1]), splat(H[4]), splat(H[7]), cx, cy, cz, py, 0, ra);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
 #pragma unroll 1
     for (int jj = 0; jj < kTaps; jj += 2) {
-        fetch_row<FAST, TX>(im, splat(H[1]), splat(H[4]), splat(H[7]), cx, cy, cz, py, jj + 1, rb);
+        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 1, rb);
         reduce_row<TX>(ra, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
-        if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, splat(H[1]), splat(H[4]), splat(H[7]), cx, cy, cz, py, jj + 2, ra);
+        if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 2, ra);
         reduce_row<TX>(rb, wl, rt, wstride, jj + 1, acc_s, acc_ss, acc_rs);
     }
     sum_src = 0.0f;
@@ -674,29 +661,14 @@ DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px
     ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
-constexpr float kCostMax = 2.0f, kMinVar = 1e-5f;
-
-// The tail of ComputeBilateralNCC (src/ACMMP.cu:413-431) from the three
-// weighted source sums.
-DEV float ncc_finish(const PixPatch &pp, float sum_src, float sum_ss, float sum_rs) {
-    sum_src *= pp.inv_wsum;
-    const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
-    if (var_src < kMinVar) return kCostMax;
-    const float covar = dm_fma(sum_rs, pp.inv_wsum, -(pp.mean * sum_src));
-    const float var_rs = dm_sqrt(pp.var * var_src);
-    float c = 1.0f - covar / var_rs;
-    c = (c < kCostMax) ? c : kCostMax;
-    c = (c > 0.0f) ? c : 0.0f;
-    return c;
-}
-
 // ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
 // wave-uniform). Reference samples come from the LDS tile, source samples
 // through ncc_sums.
 template <int TX>
 DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
                         int py, float4 h) {
-    const float cost_max = kCostMax;
+    const float cost_max = 2.0f;
+    const float kMinVar = 1e-5f;
     // var_ref is invariant: when it is below kMinVar (or the centre maps
     // outside the source) every call returns cost_max.
     if (pp.var < kMinVar) return cost_max;
@@ -720,229 +692,15 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
     if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-    return ncc_finish(pp, sum_src, sum_ss, sum_rs);
-}
-
-// ------------------------------------------------- pipelined NCC streams
-// A run of NCC calls with a wave-uniform view per call (Phase A: (view,
-// candidate) in the reference's order, src/ACMMP.cu:806-812) evaluated as
-// ONE software pipeline over the calls' patch rows: while the current
-// call's last row is in flight, the next call's homography is formed and its
-// first row of gathers issued, so no call starts on an exposed gather
-// latency (a call used to restart the two-row pipeline of ncc_sums_rows).
-// Per call and lane the operations and their order are bilateral_ncc's, so
-// every result is bit-identical; a lane whose call returns early (inactive,
-// var_ref < kMinVar, centre outside the source) runs the rows on a benign
-// homography (u = v = 0: record 0, always in bounds) and takes its constant.
-// The reciprocal form is chosen per call for the whole wave: the Newton form
-// when every running lane's patch is inside its window (bit-identical to the
-// IEEE division there), the IEEE division otherwise (exact for every lane).
-template <int TX>
-struct NccJob {
-    SrcImage im;                             // wave-uniform view
-    f2v cx[kPairs], cy[kPairs], cz[kPairs];  // column terms of pin P1
-    f2v h1, h4, h7;                          // row terms, as register pairs (see ncc_prep)
-    float cres;                              // this lane's result when !run
-    bool run;                                // this lane's NCC runs
-    bool fast;                               // wave-uniform: Newton reciprocal for the call
-    bool any;                                // wave-uniform: some lane runs
-};
-
-template <int TX>
-DEV void ncc_prep(const KViews &kv, const PixPatch &pp, int v, float4 h, int px, int py, bool active, float idle,
-                  NccJob<TX> &J) {
-    J.im = src_image<TX>(kv, v);
-    bool run = active && !(pp.var < kMinVar);
-    J.cres = active ? kCostMax : idle;
-    float H[9];
-    homography(kv, v, h, H);
-    const float2 pt = project(H, (float)px, (float)py);
-    if (pt.x >= (float)J.im.W || pt.x < 0.0f || pt.y >= (float)J.im.H || pt.y < 0.0f) run = false;
-    const float xl = (float)(px - 5), xr = (float)(px + 5), yt = (float)(py - 5), yb = (float)(py + 5);
-    const float z00 = dm_fma(H[7], yt, dm_fma(H[6], xl, H[8]));
-    const float z10 = dm_fma(H[7], yt, dm_fma(H[6], xr, H[8]));
-    const float z01 = dm_fma(H[7], yb, dm_fma(H[6], xl, H[8]));
-    const float z11 = dm_fma(H[7], yb, dm_fma(H[6], xr, H[8]));
-    const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
-    const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
-    const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-    J.run = run;
-    J.any = __ballot(run) != 0;
-    J.fast = __ballot(run && !fast) == 0;
-    if (!run) {  // benign homography: every sample at (0, 0)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) H[i] = 0.0f;
-        H[8] = 1.0f;
-    }
-    int xoff = 0;
-#if ACMMP_UB_SHARE > 1
-    // TIMING-ONLY upper bound (wrong results): the lanes of a
-    // TD group (even or odd lanes of a 16-lane quarter-wave) form subgroups
-    // of ACMMP_UB_SHARE lanes that gather with their leader's homography and
-    // pixel, sub-rank r shifted by about 6 r / SHARE patch columns -- the
-    // address pattern of SHARE lanes splitting one pixel's patch columns.
-    // VALU per lane is unchanged, so the bound measures TD relief alone.
-    {
-        const int lane = __lane_id();
-        const int rank = (lane >> 1) & 7, sub = ACMMP_UB_SHARE > 8 ? 0 : rank & (ACMMP_UB_SHARE - 1);
-        // SHARE 64: every lane on lane 0's pixel and columns (a probe of the cost model)
-        const int leader = ACMMP_UB_SHARE > 8 ? 0 : (lane & ~0xF) | (lane & 1) | ((rank & ~(ACMMP_UB_SHARE - 1)) << 1);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) H[i] = __shfl(H[i], leader);
-        const int lpx = __shfl(px, leader), dy = __shfl(py, leader) - py;
-        xoff = lpx - px + 2 * ((6 * sub) / ACMMP_UB_SHARE);
-        // the rows use this lane's py: fold the leader's row offset into the
-        // constant terms (H[2], H[5], H[8] move with y)
-        H[2] += H[1] * (float)dy;
-        H[5] += H[4] * (float)dy;
-        H[8] += H[7] * (float)dy;
-    }
-#endif
-    // the row terms as genuine register pairs: a splat the compiler can see
-    // becomes one register read through op_sel, and the wait-count pass then
-    // treats the (unused) neighbour register as read, so a gather whose
-    // destination lands there is waited on before the next row's arithmetic
-    J.h1 = splat(H[1]);
-    J.h4 = splat(H[4]);
-    J.h7 = splat(H[7]);
-    asm volatile("" : "+v"(J.h1), "+v"(J.h4), "+v"(J.h7));
-#pragma unroll
-    for (int p = 0; p < kPairs; ++p) {
-        const f2v x = f2v{(float)(px - 5 + 4 * p + xoff), (float)(px - 3 + 4 * p + xoff)};
-        J.cx[p] = fma2(splat(H[0]), x, splat(H[2]));
-        J.cy[p] = fma2(splat(H[3]), x, splat(H[5]));
-        J.cz[p] = fma2(splat(H[6]), x, splat(H[8]));
-    }
-}
-
-// Always the Newton form: a call with a lane outside the reciprocal window
-// (J.fast false, rare) is recomputed whole by bilateral_ncc afterwards; its
-// pipelined gathers only need to stay in bounds, which the clamp and the
-// buffer's record bound guarantee for any value. (Choosing the form per row
-// instead puts a branch diamond around every fetch, and the wait-count pass
-// then drains every load before each row.)
-template <int TX>
-DEV void ncc_fetch(const NccJob<TX> &J, int py, int jj, RowFetch<TX> &rf) {
-    fetch_row<true, TX>(J.im, J.h1, J.h4, J.h7, J.cx, J.cy, J.cz, py, jj, rf);
-}
-
-// column totals in the pinned order (ncc_sums_rows)
-DEV void ncc_totals(const f2v *acc_s, const f2v *acc_ss, const f2v *acc_rs, float &sum_src, float &sum_ss,
-                    float &sum_rs) {
-    sum_src = 0.0f;
-    sum_ss = 0.0f;
-    sum_rs = 0.0f;
-#pragma unroll
-    for (int p = 0; p < kPairs; ++p) {
-        sum_src += acc_s[p].x;
-        sum_src += acc_s[p].y;
-        sum_ss += acc_ss[p].x;
-        sum_ss += acc_ss[p].y;
-        sum_rs += acc_rs[p].x;
-        sum_rs += acc_rs[p].y;
-    }
-}
-
-// Keeps a row's accumulation where it is written: without it the compiler
-// sinks every row's reduction below the call's last fetch (the sums are only
-// read at the end), so all 36 gathers are waited on together and the next
-// call's prologue cannot overlap anything. Emits no instruction.
-DEV void pin_acc(f2v *acc_s, f2v *acc_ss, f2v *acc_rs) {
-#pragma unroll
-    for (int p = 0; p < kPairs; ++p) asm volatile("" : "+v"(acc_s[p]), "+v"(acc_ss[p]), "+v"(acc_rs[p]));
-}
-
-// Runs `njobs` NCC calls as one pipeline. job(k, J) prepares call k
-// (ncc_prep with its view, plane and activity); exact(k) is call k by
-// bilateral_ncc; done(k, c) receives call k's cost, in order k = 0, 1, ...
-// A call joins the pipeline when some lane runs it and every running lane is
-// inside the Newton window (nearly all calls); any other call is finished on
-// the spot (its constants, or bilateral_ncc, which takes the IEEE division
-// where needed) with nothing in flight. Every path issues the same loads in
-// the same order: the wait-count pass aligns merged paths at their last load,
-// so a path with fewer loads would make the next wait drain everything.
-template <int TX, typename JOB, typename EXACT, typename DONE>
-DEV void ncc_stream(const PixPatch &pp, int py, int njobs, bool pipe, JOB job, EXACT exact, DONE done) {
-    int wo = pp.wo;
-    RowFetch<TX> ra, rb;
-    NccJob<TX> J;
-    int k = 0;
-    // calls outside the pipeline, from k on; leaves J prepared for call k
-    auto direct = [&]() {
-        while (k < njobs && !(J.fast && J.any)) {
-            float c = J.cres;
-            if (!J.fast && J.run) c = exact(k);
-            done(k, c);
-            if (++k < njobs) job(k, J);
-        }
-    };
-    job(0, J);
-    direct();
-    ncc_fetch<TX>(J, py, 0, ra);
-#pragma unroll 1
-    while (k < njobs) {
-        // the weight slots are re-read from LDS each call (ncc_sums)
-        asm volatile("" : "+v"(wo));
-        const WSlot *wl = pp.w - pp.wo + wo;
-        f2v acc_s[kPairs], acc_ss[kPairs], acc_rs[kPairs];
-#pragma unroll
-        for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
-        const bool run = J.run;
-        ncc_fetch<TX>(J, py, 1, rb);
-        __builtin_amdgcn_sched_barrier(0);  // the row's loads go out before the previous row is reduced
-        reduce_row<TX>(ra, wl, pp.rt, kThreads, 0, acc_s, acc_ss, acc_rs);
-        pin_acc(acc_s, acc_ss, acc_rs);
-        ncc_fetch<TX>(J, py, 2, ra);
-        __builtin_amdgcn_sched_barrier(0);
-        reduce_row<TX>(rb, wl, pp.rt, kThreads, 1, acc_s, acc_ss, acc_rs);
-        pin_acc(acc_s, acc_ss, acc_rs);
-        ncc_fetch<TX>(J, py, 3, rb);
-        __builtin_amdgcn_sched_barrier(0);
-        reduce_row<TX>(ra, wl, pp.rt, kThreads, 2, acc_s, acc_ss, acc_rs);
-        pin_acc(acc_s, acc_ss, acc_rs);
-        ncc_fetch<TX>(J, py, 4, ra);
-        __builtin_amdgcn_sched_barrier(0);
-        reduce_row<TX>(rb, wl, pp.rt, kThreads, 3, acc_s, acc_ss, acc_rs);
-        pin_acc(acc_s, acc_ss, acc_rs);
-        ncc_fetch<TX>(J, py, 5, rb);
-        __builtin_amdgcn_sched_barrier(0);
-        reduce_row<TX>(ra, wl, pp.rt, kThreads, 4, acc_s, acc_ss, acc_rs);
-        pin_acc(acc_s, acc_ss, acc_rs);
-        const float cres = J.cres;
-        const bool more = k + 1 < njobs;
-        bool joins;
-        if (pipe) {
-            // the next call's prologue and first row, in flight while row 5
-            // is reduced (the last call re-prepares itself; never read)
-            job(more ? k + 1 : k, J);
-            joins = more && J.fast && J.any;
-            ncc_fetch<TX>(J, py, 0, ra);
-            __builtin_amdgcn_sched_barrier(0);
-            reduce_row<TX>(rb, wl, pp.rt, kThreads, 5, acc_s, acc_ss, acc_rs);
-            float sum_src, sum_ss, sum_rs;
-            ncc_totals(acc_s, acc_ss, acc_rs, sum_src, sum_ss, sum_rs);
-            done(k, run ? ncc_finish(pp, sum_src, sum_ss, sum_rs) : cres);
-        } else {
-            // one call at a time: the next prologue after this call is done
-            // (same loads in the same number on both paths)
-            reduce_row<TX>(rb, wl, pp.rt, kThreads, 5, acc_s, acc_ss, acc_rs);
-            float sum_src, sum_ss, sum_rs;
-            ncc_totals(acc_s, acc_ss, acc_rs, sum_src, sum_ss, sum_rs);
-            done(k, run ? ncc_finish(pp, sum_src, sum_ss, sum_rs) : cres);
-            __builtin_amdgcn_sched_barrier(0);
-            job(more ? k + 1 : k, J);
-            joins = more && J.fast && J.any;
-            ncc_fetch<TX>(J, py, 0, ra);
-        }
-        ++k;
-        if (!joins) {
-            // rare: retire the row just fetched, finish the calls that cannot
-            // join on the spot, and restart the pipeline at the next one
-            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-            direct();
-            ncc_fetch<TX>(J, py, 0, ra);
-        }
-    }
+    sum_src *= pp.inv_wsum;
+    const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
+    if (var_src < kMinVar) return cost_max;
+    const float covar = dm_fma(sum_rs, pp.inv_wsum, -(pp.mean * sum_src));
+    const float var_rs = dm_sqrt(pp.var * var_src);
+    float c = 1.0f - covar / var_rs;
+    c = (c < cost_max) ? c : cost_max;
+    c = (c > 0.0f) ? c : 0.0f;
+    return c;
 }
 
 // ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
@@ -1558,44 +1316,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     const float cost_threshold = (float)(0.8 * (double)dm_expf((float)(iter * iter) / (-90.0f)));
     // view-major: the 8 candidates of one source view gather from nearly the
     // same footprint, back to back (results are independent)
-#if ACMMP_PIPE
-    // the 8 x nsrc calls as one NCC stream (ncc_stream): each call's first
-    // patch row is in flight before the previous call's last row is reduced
-    {
-        float count = 0;
-        int count_false = 0;
-        float tmpw = 0;
-        ncc_stream<TX>(
-            pp, py, 8 * nsrc, iter >= kv.pipe_from[prm.geom_consistency ? 1 : 0],
-            [&](int k, NccJob<TX> &J) {
-                const int v = k >> 3, d = k & 7;
-                ncc_prep<TX>(kv, pp, v + 1, cand(d), px, py, (flags >> d) & 1u, (d == 0 && v == 0) ? 2.0f : 0.0f,
-                             J);
-            },
-            [&](int k) { return bilateral_ncc<TX>(kv, tile, g.tb, pp, (k >> 3) + 1, px, py, cand(k & 7)); },
-            [&](int k, float c) {
-                const int v = k >> 3, d = k & 7;
-                cost_array[d][v] = c;
-                if (c < cost_threshold) {
-                    tmpw += dm_expf(c * c / (-0.18f));
-                    count++;
-                }
-                if (c > 1.2f) count_false++;
-                if (d == 7) {  // the view's sampling statistics (:1013-1031)
-                    float vsp = 0.0f;
-                    for (int n = 0; n < 4; ++n)
-                        if ((flags >> (2 * n)) & 1u) vsp += ((nb[n] >> v) & 1u) ? 0.9f : 0.1f;
-                    float pr = 0.0f;
-                    if (count > 2 && count_false < 3) pr = tmpw / count;
-                    else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
-                    probs[v] = pr * vsp;
-                    count = 0;
-                    count_false = 0;
-                    tmpw = 0;
-                }
-            });
-    }
-#else
     for (int v = 0; v < nsrc; ++v) {
         // one NCC call site: the candidate loop stays rolled (d is wave-uniform,
         // the candidate's index is picked by selects), and the sampling
@@ -1623,19 +1343,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
         probs[v] = pr * vsp;
     }
-#endif
 
-#if ACMMP_PHASE_A_ONLY
-    // TIMING-ONLY build: Phase A alone (its costs folded into the stored cost
-    // so nothing is dead), the state otherwise unchanged
-    {
-        float acc = 0.0f;
-        for (int v = 0; v < nsrc; ++v) acc += probs[v];
-        st.plane_nx[colour][my] = my_plane;
-        st.cost_nx[colour][my] = my_cost + 0.0f * acc;
-        return;
-    }
-#endif
     // ---- multi-hypothesis joint view selection (:994-1056)
     // CDF in registers (static indices over NS, predicated on i < nsrc): the
     // 15 draws then need no dependent scratch loads. The CDF is
