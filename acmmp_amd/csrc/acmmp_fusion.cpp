@@ -562,9 +562,13 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     struct ViewHits {
         std::vector<std::vector<uint32_t>> hit;    // hits of row r, pixel order: j << kSpBits | sp
         std::vector<std::vector<float>> ex;        // their exp(-tmp_index)
-        std::vector<std::vector<uint16_t>> nhit;   // hits per pixel; 0xffff = not live
-        std::vector<std::vector<float>> sum;       // per pixel: sum of its hits' ex, ascending j
-        std::vector<std::vector<F3>> X;            // world point of each live pixel of row r, in order
+        // per live pixel of row r (phase 1's order: ascending column) --
+        // the walk visits only these (a pixel not live in phase 1 stays so:
+        // masks only go 0 -> 1 and depths do not change)
+        std::vector<std::vector<int>> live;        // its column
+        std::vector<std::vector<uint16_t>> nhit;   // its number of hits
+        std::vector<std::vector<float>> sum;       // sum of its hits' ex, ascending j
+        std::vector<std::vector<F3>> X;            // its world point
     };
     for (size_t i = 0; i < n; ++i)
         if ((size_t)cols[i] * rows[i] > (size_t(1) << kSpBits) || problems[i].num_src_images > 32)
@@ -594,8 +598,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::vector<F3> &X = vh.X[(size_t)r];
         h.clear();
         hx.clear();
-        nh.assign((size_t)W, 0xffff);
-        sum.assign((size_t)W, 0.0f);
         rs.live.clear();
         rs.X.clear();
         for (int c = 0; c < W; ++c) {
@@ -610,6 +612,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         const size_t nj = (size_t)std::max(num_ngb, 1);
         rs.sp.assign(nl * nj, kNoHit);
         rs.e.resize(nl * nj);
+        nh.resize(nl);
+        sum.resize(nl);
         for (int j = 0; j < num_ngb; ++j) {
             const int s = src_index[i][j];
             const int src_cols = cols[s], src_rows = rows[s];
@@ -657,18 +661,20 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 hx.push_back(e);
                 total += e;
             }
-            nh[(size_t)rs.live[k]] = (uint16_t)(h.size() - k0);
-            sum[(size_t)rs.live[k]] = total;
+            nh[k] = (uint16_t)(h.size() - k0);
+            sum[k] = total;
         }
         // the walk emits an approved pixel's point from here (the same
         // world_point call the reference makes at approval, :1012)
         X.swap(rs.X);
+        vh.live[(size_t)r].swap(rs.live);
     };
     std::vector<ViewHits> vhits(2);
     auto start_phase1 = [&](size_t i) {
         ViewHits &vh = vhits[i & 1];
         vh.hit.resize((size_t)rows[i]);
         vh.ex.resize((size_t)rows[i]);
+        vh.live.resize((size_t)rows[i]);
         vh.nhit.resize((size_t)rows[i]);
         vh.sum.resize((size_t)rows[i]);
         vh.X.resize((size_t)rows[i]);
@@ -705,24 +711,27 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         for (int r = 0; r < H; ++r) {
             const uint32_t *h = vh.hit[(size_t)r].data();
             const float *hx = vh.ex[(size_t)r].data();
+            const std::vector<int> &lv = vh.live[(size_t)r];
             const uint16_t *nhr = vh.nhit[(size_t)r].data();
             const float *sumr = vh.sum[(size_t)r].data();
             const F3 *xr = vh.X[(size_t)r].data();
-            for (int c = 0; c < W; ++c) {
+            const size_t nl = lv.size();
+            for (size_t k = 0; k < nl; ++k) {  // the pixels live in phase 1, in column order
+                const int c = lv[k];
                 const size_t pc = (size_t)r * W + c;
-                const int nh = nhr[c];
-                if (nh == 0xffff) continue;
+                const int nh = nhr[k];
                 const uint32_t *hp = h;
                 const float *hxp = hx;
-                const F3 *xp = xr++;
+                const F3 *xp = xr + k;
                 h += nh;
                 hx += nh;
-                // masks[i] changes during view i only if i is its own source
+                // re-read: view i - 1's walk (beside view i's phase 1) and,
+                // if i is its own source, view i's own approvals set bits
                 if (masks[i].get(pc)) continue;
                 int num_consistent = 0;
                 bool masked = false;
-                for (int k = 0; k < nh; ++k) {
-                    const uint32_t j = hp[k] >> kSpBits, sp = hp[k] & kSpMask;
+                for (int q = 0; q < nh; ++q) {
+                    const uint32_t j = hp[q] >> kSpBits, sp = hp[q] & kSpMask;
                     if (bit(mw[j], sp)) {
                         masked = true;
                         continue;
@@ -731,14 +740,14 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                     dirty |= 1u << j;
                     num_consistent++;
                 }
-                float dynamic_consistency = sumr[c];
+                float dynamic_consistency = sumr[k];
                 n_live++;
                 n_hits += (size_t)nh;
                 n_masked += masked;
                 if (masked) {  // re-add the unmasked ones, ascending j
                     dynamic_consistency = 0;
-                    for (int k = 0; k < nh; ++k)
-                        if (!bit(mw[hp[k] >> kSpBits], hp[k] & kSpMask)) dynamic_consistency += hxp[k];
+                    for (int q = 0; q < nh; ++q)
+                        if (!bit(mw[hp[q] >> kSpBits], hp[q] & kSpMask)) dynamic_consistency += hxp[q];
                 }
                 if (num_consistent >= con_num_thresh && (dynamic_consistency > consistency_scalar * num_consistent)) {
                     const float *ref_normal = &normals[i][pc * 3];
