@@ -263,6 +263,24 @@ struct MaskBits {
     }
 };
 
+// Runs fn(0..n-1) on the pool's workers (the caller waits); returns the
+// status of the lowest failing index with its message, as parallel_for does.
+template <class Fn>
+int pool_for(Pool &pool, int n, Fn fn) {
+    std::vector<int> rc((size_t)std::max(n, 0), ACMMP_OK);
+    std::vector<std::string> msg(rc.size());
+    pool.wait(pool.submit(n, [&](int i) {
+        rc[(size_t)i] = fn(i);
+        if (rc[(size_t)i]) msg[(size_t)i] = f_err;
+    }));
+    for (int i = 0; i < n; ++i)
+        if (rc[(size_t)i]) {
+            f_err = msg[(size_t)i];
+            return rc[(size_t)i];
+        }
+    return ACMMP_OK;
+}
+
 // Runs fn(0..n-1) on acmmp_host_threads() threads; returns the status of the lowest
 // failing index with its message (what the sequential loop reports first).
 template <class Fn>
@@ -477,8 +495,16 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     const auto t_start = now();
     double t_wait = 0, t_walk = 0;
     size_t n_live = 0, n_hits = 0, n_masked = 0;
+    // The threads are confined to one last-level-cache domain BEFORE the
+    // loads, and the loads run on that domain's pool: the maps, images and
+    // masks are then first touched (allocated) on the memory node of the
+    // walk's core, which reads them. (Loaded by threads spread over the whole
+    // machine, a 2-socket host put part of them on the other node, and the
+    // walk measured 0.85 or 1.3 s from run to run, profiles/r05_fusion_walk_ab3.jsonl.)
+    CacheDomain dom;
+    Pool pool(&dom);
     // views load independently (JPEG decode, two .dmb reads, optional mask)
-    int load_rc = parallel_for((int)n, [&](int vi) -> int {
+    int load_rc = pool_for(pool, (int)n, [&](int vi) -> int {
         const size_t i = (size_t)vi;
         const int id = problems[i].ref_image_id;
         const std::string ipath = image_folder + "/" + id8(id) + ".jpg";
@@ -544,8 +570,6 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                              problems[i].ref_image_id);
             src_index[i].push_back(it->second);
         }
-    CacheDomain dom;  // after the loads, which use every allowed CPU
-    Pool pool(&dom);
     // Two phases per view, exact to the sequential loop: (1) on the pool,
     // every pixel's per-source projections and consistency tests against
     // the masks as they stand (masks only ever go 0 -> 1, so a source or
