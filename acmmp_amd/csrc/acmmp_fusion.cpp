@@ -608,6 +608,12 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         std::vector<int> live;           // columns of the live pixels
         std::vector<uint32_t> sp;        // [live k][j]: source pixel of a hit, or kNoHit
         std::vector<float> e;            // [live k][j]: its exp(-tmp_index)
+        // one source's pass over the row, in stages (see phase1)
+        std::vector<int> src_c, src_r;   // [live k]: the projected source pixel
+        std::vector<int> cand;           // live indices whose source pixel is in bounds, unmasked, depth > 0
+        std::vector<int> ccol, csc, csr; // ... its column and source pixel
+        std::vector<float> cdepth, cref; // ... its source depth and reference depth
+        std::vector<float> rerr, rdiff;  // [cand q]: reprojection error, relative depth difference
     };
     constexpr uint32_t kNoHit = 0xffffffffu;
     auto phase1 = [&](size_t i, ViewHits &vh, int r) {
@@ -638,39 +644,85 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         rs.e.resize(nl * nj);
         nh.resize(nl);
         sum.resize(nl);
+        rs.src_c.resize(nl);
+        rs.src_r.resize(nl);
         for (int j = 0; j < num_ngb; ++j) {
             const int s = src_index[i][j];
             const int src_cols = cols[s], src_rows = rows[s];
+            // Per source, the reference's per-pixel test in four stages over
+            // the row's live pixels (the same operations on the same values:
+            // the two arithmetic stages are branch-free loops the compiler
+            // vectorises; the gathers and the mask reads stay scalar).
+            // (1) the projection into the source
+            {
+                const F3 *X = rs.X.data();
+                int *scp = rs.src_c.data(), *srp = rs.src_r.data();
+                const acmmp_camera &cs = cameras[s];
+                for (size_t k = 0; k < nl; ++k) {
+                    float ptx, pty, proj_depth;
+                    project(X[k], cs, ptx, pty, proj_depth);
+                    srp[k] = int(pty + 0.5f);
+                    scp[k] = int(ptx + 0.5f);
+                }
+            }
+            // (2) in bounds, unmasked, positive source depth: the candidates,
+            // with what stage 3 reads, in contiguous arrays
+            rs.cand.resize(nl);
+            rs.ccol.resize(nl);
+            rs.csc.resize(nl);
+            rs.csr.resize(nl);
+            rs.cdepth.resize(nl);
+            rs.cref.resize(nl);
+            size_t nc = 0;
+            const float *dref = depths[i].data() + (size_t)r * W;
             for (size_t k = 0; k < nl; ++k) {
-                const int c = rs.live[k];
-                const size_t pc = (size_t)r * W + c;
-                const float ref_depth = depths[i][pc];
-                const float *ref_normal = &normals[i][pc * 3];
-                float ptx, pty, proj_depth;
-                project(rs.X[k], cameras[s], ptx, pty, proj_depth);
-                const int src_r = int(pty + 0.5f);
-                const int src_c = int(ptx + 0.5f);
+                const int src_r = rs.src_r[k], src_c = rs.src_c[k];
                 if (!(src_c >= 0 && src_c < src_cols && src_r >= 0 && src_r < src_rows)) continue;
                 const size_t sp = (size_t)src_r * src_cols + src_c;
                 if (masks[s].get(sp)) continue;
                 const float src_depth = depths[s][sp];
-                const float *src_normal = &normals[s][sp * 3];
                 if (src_depth <= 0.0) continue;
-                const F3 tmp_X = world_point(src_c, src_r, src_depth, cameras[s]);
-                float tx, ty;
-                project(tmp_X, cameras[i], tx, ty, proj_depth);
-                // std::pow(v, 2) of a float v is exact in double: v * v
-                const double dx = (double)(c - tx), dy = (double)(r - ty);
-                const float reproj_error = (float)std::sqrt(dx * dx + dy * dy);
-                const float relative_depth_diff = std::fabs(proj_depth - ref_depth) / ref_depth;
-                // the reference evaluates all three before the test; acos is
-                // pure, so it is only needed where the first two pass
+                rs.cand[nc] = (int)k;
+                rs.ccol[nc] = rs.live[k];
+                rs.csc[nc] = src_c;
+                rs.csr[nc] = src_r;
+                rs.cdepth[nc] = src_depth;
+                rs.cref[nc] = dref[rs.live[k]];
+                ++nc;
+            }
+            // (3) the reprojection into view i: error and relative depth difference
+            rs.rerr.resize(nc);
+            rs.rdiff.resize(nc);
+            {
+                const int *__restrict__ col = rs.ccol.data(), *__restrict__ scp = rs.csc.data();
+                const int *__restrict__ srp = rs.csr.data();
+                const float *__restrict__ cd = rs.cdepth.data(), *__restrict__ cr = rs.cref.data();
+                float *__restrict__ re = rs.rerr.data(), *__restrict__ rd = rs.rdiff.data();
+                const acmmp_camera cs = cameras[s], ci = cameras[i];
+                for (size_t q = 0; q < nc; ++q) {
+                    const float ref_depth = cr[q];
+                    float tx, ty, proj_depth;
+                    const F3 tmp_X = world_point(scp[q], srp[q], cd[q], cs);
+                    project(tmp_X, ci, tx, ty, proj_depth);
+                    // std::pow(v, 2) of a float v is exact in double: v * v
+                    const double dx = (double)(col[q] - tx), dy = (double)(r - ty);
+                    re[q] = (float)std::sqrt(dx * dx + dy * dy);
+                    rd[q] = std::fabs(proj_depth - ref_depth) / ref_depth;
+                }
+            }
+            // (4) the reference evaluates all three before the test; acos is
+            // pure, so the angle is only formed where the first two pass
+            for (size_t q = 0; q < nc; ++q) {
+                const float reproj_error = rs.rerr[q], relative_depth_diff = rs.rdiff[q];
                 if (!(reproj_error < 2.0f && relative_depth_diff < 0.01f)) continue;
-                const float angle = get_angle(ref_normal, src_normal);
+                const int k = rs.cand[q];
+                const size_t pc = (size_t)r * W + rs.ccol[q];
+                const size_t sp = (size_t)rs.csr[q] * src_cols + rs.csc[q];
+                const float angle = get_angle(&normals[i][pc * 3], &normals[s][sp * 3]);
                 if (angle < 0.174533f) {
                     const float tmp_index = reproj_error + 200 * relative_depth_diff + angle * 10;
-                    rs.sp[k * nj + (size_t)j] = (uint32_t)sp;
-                    rs.e[k * nj + (size_t)j] = std::exp(-tmp_index);
+                    rs.sp[(size_t)k * nj + (size_t)j] = (uint32_t)sp;
+                    rs.e[(size_t)k * nj + (size_t)j] = std::exp(-tmp_index);
                 }
             }
         }

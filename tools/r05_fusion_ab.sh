@@ -6,4 +6,4 @@
 export TMPDIR=/tmp
 V=acmmp_amd/lib/variants
 bash tools/gpu_steps.sh \
- "700 python3 tools/fusion_ab.py '[{\"ACMMP_LIB\": \"$V/libacmmp_amd_fwp.so\"}, {}]' 11 > gpurun_out/fusion_ab4.jsonl"
+ "700 python3 tools/fusion_ab.py '[{\"ACMMP_LIB\": \"$V/libacmmp_amd_fwp.so\"}, {}]' 11 > gpurun_out/fusion_ab5.jsonl"
