@@ -49,10 +49,6 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
-// Phase A: a candidate identical to an earlier one copies its cost (A/B builds: 0 = off)
-#ifndef ACMMP_DUP_SKIP
-#define ACMMP_DUP_SKIP 1
-#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -1296,27 +1292,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 #pragma unroll
     for (int d = 0; d < 8; ++d) cand_slot[d * kThreads] = cpl[d];
     auto cand = [&](int d) -> float4 { return cand_slot[d * kThreads]; };
-    // A flagged candidate whose plane equals an earlier flagged candidate's bit
-    // for bit has the same NCC for every view (same pixel, plane, view): its
-    // lane copies that cost instead of running the call (4 bits per d: the
-    // earlier candidate, 15 = none). The wave still runs the call for its
-    // other lanes, but the idle lanes' gathers cost no texture-path accesses.
-    uint32_t dupmap = 0xffffffffu;
-#if ACMMP_DUP_SKIP
-#pragma unroll
-    for (int d = 1; d < 8; ++d) {
-        uint32_t src = 15u;
-#pragma unroll
-        for (int e = d - 1; e >= 0; --e) {
-            const bool same = __float_as_uint(cpl[d].x) == __float_as_uint(cpl[e].x) &&
-                              __float_as_uint(cpl[d].y) == __float_as_uint(cpl[e].y) &&
-                              __float_as_uint(cpl[d].z) == __float_as_uint(cpl[e].z) &&
-                              __float_as_uint(cpl[d].w) == __float_as_uint(cpl[e].w);
-            if (same && ((flags >> e) & 1u)) src = (uint32_t)e;
-        }
-        dupmap &= ~(15u << (4 * d)) | (src << (4 * d));
-    }
-#endif
 
     PixPatch pp;
     pp.wo = threadIdx.y * kBX + threadIdx.x;
@@ -1351,9 +1326,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 #pragma unroll 1
         for (int d = 0; d < 8; ++d) {
             float c;
-            const uint32_t dsrc = (dupmap >> (4 * d)) & 15u;
-            if (((flags >> d) & 1u) && dsrc == 15u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
-            else if ((flags >> d) & 1u) c = cost_array[dsrc][v];  // an identical earlier plane's cost
+            if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
             else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
             cost_array[d][v] = c;
             if (c < cost_threshold) {
