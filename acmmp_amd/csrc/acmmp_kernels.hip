@@ -333,7 +333,12 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #ifndef ACMMP_KBX
 #define ACMMP_KBX 16
 #endif
-constexpr int kBX = ACMMP_KBX, kBY = 256 / kBX;  // ACMMP_KBX: A/B builds only
+// threads per block of the colour-split kernels (A/B builds: 512 puts a CU's
+// eight waves in one block, i.e. on adjacent pixels)
+#ifndef ACMMP_BLOCK_THREADS
+#define ACMMP_BLOCK_THREADS 256
+#endif
+constexpr int kBX = ACMMP_KBX, kBY = ACMMP_BLOCK_THREADS / kBX;  // ACMMP_KBX: A/B builds only
 constexpr int kTileW = kBX + 6, kTileH = kBY + 10;
 
 DEV void load_ref_tile(const KViews &kv, float *tile, int k0, int y0, int colour) {
@@ -967,7 +972,7 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, t
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
 // writes the colour-split "current" buffers. blockIdx.z = colour.
 template <int NS, int TX>
-__global__ __launch_bounds__(256) void k_init(const KViews *__restrict__ kvp, KState st) {
+__global__ __launch_bounds__(ACMMP_BLOCK_THREADS) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
@@ -1657,7 +1662,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 }
 
 template <int NS, int TX>
-__global__ __launch_bounds__(256, kSweepWaves) void k_sweep_f(const KViews *__restrict__ kvp, KState st, int colour,
+__global__ __launch_bounds__(ACMMP_BLOCK_THREADS, kSweepWaves) void k_sweep_f(const KViews *__restrict__ kvp, KState st, int colour,
                                                               int iter) {
     sweep_body<NS, TX>(kvp, st, colour, iter);
 }
@@ -1665,7 +1670,7 @@ __global__ __launch_bounds__(256, kSweepWaves) void k_sweep_f(const KViews *__re
 // T1 kernel: costs of a given plane per pixel against every source view
 // (same NCC code path as the sweep; blockIdx.z = colour).
 template <int NS, int TX>
-__global__ __launch_bounds__(256) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
+__global__ __launch_bounds__(ACMMP_BLOCK_THREADS) void k_eval_costs(const KViews *__restrict__ kvp, const float4 *planes,
                                                     float *out, float *out_init, uint32_t *out_views) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
