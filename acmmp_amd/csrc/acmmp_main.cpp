@@ -41,6 +41,8 @@ void usage() {
         "  --multi_fusion [DIR]     with -p: prior-aware fusion against <dense>DIR (default /ACMMP)\n"
         "  --force_fusion           prior-aware fusion even without -p\n"
         "  --single_match_penalty N extra consistent views required of one-sided support (0)\n"
+        "  --order sequential|jacobi  pass order: the reference's (default; a geometric pass reads the maps\n"
+        "                           of the views before it in the same pass) or Jacobi (= --view_parallel)\n"
         "  --view_parallel          multi-GPU: one process per GPU (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/\n"
         "                           MASTER_PORT from the environment, e.g. torchrun --no-python), views\n"
         "                           sharded per pass, depth maps all-gathered (Jacobi order); rank 0 fuses\n"
@@ -89,6 +91,16 @@ int main(int argc, char **argv) {
             device_set = true;
         } else if (a == "--view_parallel") {
             view_parallel = true;
+        } else if (a == "--order" || a.rfind("--order=", 0) == 0) {
+            // one GPU offers both pass orders; jacobi = the
+            // view-parallel driver at world 1 (every view of a pass reads the
+            // previous pass's maps), sequential = the reference's order
+            const std::string o = a == "--order" ? value() : a.substr(8);
+            if (o != "sequential" && o != "jacobi") {
+                std::fprintf(stderr, "acmmp_main: --order sequential|jacobi\n");
+                return 2;
+            }
+            view_parallel = o == "jacobi";
         } else if (a == "--exchange") {
             const std::string e = value();
             if (e != "rccl" && e != "tcp") {

@@ -164,3 +164,16 @@ int main() {
                     "-Wl,-rpath," + lib, "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     assert out == ["3", "0", "4", "1"]
+
+
+def test_cli_order_flag_validated():
+    """`acmmp_main --order sequential|jacobi`: a bad value is
+    a usage error (exit 2) before any device is touched."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "acmmp_amd", "lib", "acmmp_main")
+    if not os.path.exists(exe):
+        pytest.skip("acmmp_main not built")
+    r = subprocess.run([exe, "--order", "sideways", "/nonexistent"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "--order sequential|jacobi" in r.stderr
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert "--order sequential|jacobi" in r.stdout + r.stderr

@@ -66,6 +66,16 @@ def test_world1_rccl_matches_oracle_jacobi(dense, jacobi_maps):
     assert _compare(dense + "/CVP1", jacobi_maps) == 5 * 4
 
 
+def test_order_jacobi_on_one_gpu_matches_oracle(dense, jacobi_maps):
+    """a one-GPU run offers both pass orders; `--order jacobi`
+    (no launcher, no rank environment) gives the Jacobi pipeline's maps."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([EXE, dense, "--order", "jacobi", "--output_dir", "/CVPO", "--no_fusion", "--quiet"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _compare(dense + "/CVPO", jacobi_maps) == 5 * 4
+
+
 @pytest.mark.parametrize("split", [True, False])
 def test_world2_tcp_matches_oracle_jacobi_and_fuses(dense, jacobi_maps, split):
     """5 views on 2 ranks: by default the 5th is computed by both ranks as
