@@ -17,7 +17,9 @@
 // with a float bilinear filter (cv::resize's 8-bit fixed-point path is
 // unpinned).
 #include <sched.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -353,34 +355,58 @@ struct Point {
     F3 coord, normal, color;
 };
 
-int store_ply(const std::string &path, const std::vector<Point> &pc) {  // StoreColorPlyFileBinaryPointCloud
-    FILE *f = std::fopen(path.c_str(), "wb");
-    if (!f) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
-    std::fprintf(f, "ply\nformat binary_little_endian 1.0\nelement vertex %d\n", (int)pc.size());
-    std::fprintf(f, "property float x\nproperty float y\nproperty float z\n");
-    std::fprintf(f, "property float nx\nproperty float ny\nproperty float nz\n");
-    std::fprintf(f, "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n");
-    // 27-byte records (6 floats + r, g, b) assembled in one buffer, one write
-    constexpr size_t kRec = 6 * sizeof(float) + 3;
-    std::vector<char> buf(pc.size() * kRec);
-    char *o = buf.data();
-    for (const Point &p : pc) {
-        F3 X = p.coord;
-        const char b = (char)(int)p.color.x, g = (char)(int)p.color.y, r = (char)(int)p.color.z;
-        if (!(X.x < FLT_MAX && X.x > -FLT_MAX) || !(X.y < FLT_MAX && X.y > -FLT_MAX) ||
-            !(X.z < FLT_MAX && X.z >= -FLT_MAX)) {
-            X.x = X.y = X.z = 0.0f;
-        }
-        const float v[6] = {X.x, X.y, X.z, p.normal.x, p.normal.y, p.normal.z};
-        std::memcpy(o, v, sizeof(v));
-        o[24] = r;
-        o[25] = g;
-        o[26] = b;
-        o += kRec;
+// StoreColorPlyFileBinaryPointCloud. The 27-byte records (6 floats + r, g, b)
+// are formed in chunks of kPlyChunk points, each written at its own offset:
+// on the pool's workers when one is given (RunFusion's pool is idle by then),
+// else in order on the caller. Same bytes either way.
+constexpr size_t kPlyRec = 6 * sizeof(float) + 3, kPlyChunk = size_t(1) << 18;
+
+int pwrite_all(int fd, const char *p, size_t n, off_t at) {
+    while (n) {
+        const ssize_t w = ::pwrite(fd, p, n, at);
+        if (w <= 0) return -1;
+        p += w, n -= (size_t)w, at += w;
     }
-    const bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
-    if (std::fclose(f) != 0 || !ok) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
-    return ACMMP_OK;
+    return 0;
+}
+
+int store_ply(const std::string &path, const std::vector<Point> &pc, Pool *pool = nullptr) {
+    char hdr[512];
+    const int hl = std::snprintf(hdr, sizeof(hdr),
+                                 "ply\nformat binary_little_endian 1.0\nelement vertex %d\n"
+                                 "property float x\nproperty float y\nproperty float z\n"
+                                 "property float nx\nproperty float ny\nproperty float nz\n"
+                                 "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n",
+                                 (int)pc.size());
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    const int nchunks = (int)((pc.size() + kPlyChunk - 1) / kPlyChunk);
+    auto chunk = [&](int c) -> int {
+        const size_t b = (size_t)c * kPlyChunk, e = std::min(pc.size(), b + kPlyChunk);
+        std::vector<char> buf((e - b) * kPlyRec);
+        char *o = buf.data();
+        for (size_t k = b; k < e; ++k, o += kPlyRec) {
+            const Point &p = pc[k];
+            F3 X = p.coord;
+            if (!(X.x < FLT_MAX && X.x > -FLT_MAX) || !(X.y < FLT_MAX && X.y > -FLT_MAX) ||
+                !(X.z < FLT_MAX && X.z >= -FLT_MAX)) {
+                X.x = X.y = X.z = 0.0f;
+            }
+            const float v[6] = {X.x, X.y, X.z, p.normal.x, p.normal.y, p.normal.z};
+            std::memcpy(o, v, sizeof(v));
+            o[24] = (char)(int)p.color.z;  // colour is stored b, g, r; written r, g, b
+            o[25] = (char)(int)p.color.y;
+            o[26] = (char)(int)p.color.x;
+        }
+        if (pwrite_all(fd, buf.data(), buf.size(), (off_t)(hl + b * kPlyRec)))
+            return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+        return ACMMP_OK;
+    };
+    int rc = pwrite_all(fd, hdr, (size_t)hl, 0) ? ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str()) : ACMMP_OK;
+    if (rc == ACMMP_OK && pool) rc = pool_for(*pool, nchunks, chunk);
+    for (int c = 0; rc == ACMMP_OK && !pool && c < nchunks; ++c) rc = chunk(c);
+    if (::close(fd) != 0 && rc == ACMMP_OK) rc = ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
+    return rc;
 }
 
 // ---- prior-aware fusion helpers (src/acmmp_definitions.cpp:443-571)
@@ -510,11 +536,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
         const std::string ipath = image_folder + "/" + id8(id) + ".jpg";
         int iw = 0, ih = 0;
         std::vector<uint8_t> img;
-        int rc = acmmp_read_image_bgr(ipath.c_str(), nullptr, 0, &iw, &ih);
-        if (rc == ACMMP_ERR_ARG) {
-            img.resize((size_t)iw * ih * 3);
-            rc = acmmp_read_image_bgr(ipath.c_str(), img.data(), img.size(), &iw, &ih);
-        }
+        int rc = acmmp_internal_read_image_bgr(ipath.c_str(), img, iw, ih);
         if (rc) return ffail(rc, "cannot read image %s", ipath.c_str());
         const std::string cpath = cam_folder + "/" + id8(id) + "_cam.txt";
         if (acmmp_read_camera(cpath.c_str(), &cameras[i])) return ffail(ACMMP_ERR_IO, "cannot read %s", cpath.c_str());
@@ -862,7 +884,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
     }
     if (num_points) *num_points = (int)cloud.size();
     const auto t_walked = now();
-    const int rc = store_ply(out + "/ACMMP_model.ply", cloud);
+    const int rc = store_ply(out + "/ACMMP_model.ply", cloud, &pool);
     if (timing)
         std::fprintf(stderr,
                      "[RunFusion] load=%.2fs candidates_wait=%.2fs walk=%.2fs ply=%.2fs threads=%d "
@@ -897,11 +919,7 @@ int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_fo
         const std::string ipath = dense + "/images/" + id8(id) + ".jpg";
         int iw = 0, ih = 0;
         std::vector<uint8_t> img;
-        int rc = acmmp_read_image_bgr(ipath.c_str(), nullptr, 0, &iw, &ih);
-        if (rc == ACMMP_ERR_ARG) {
-            img.resize((size_t)iw * ih * 3);
-            rc = acmmp_read_image_bgr(ipath.c_str(), img.data(), img.size(), &iw, &ih);
-        }
+        int rc = acmmp_internal_read_image_bgr(ipath.c_str(), img, iw, ih);
         if (rc) return ffail(rc, "cannot read image %s", ipath.c_str());
         const std::string cpath = dense + "/cams/" + id8(id) + "_cam.txt";
         if (acmmp_read_camera(cpath.c_str(), &in.cameras[i]))

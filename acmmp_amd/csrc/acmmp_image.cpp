@@ -57,6 +57,11 @@ struct Huff {
     // 8-bit lookahead: for the next 8 bits of the stream, the length (0 = the
     // code is longer than 8 bits) and symbol of the code they start with
     uint8_t look_len[256], look_sym[256];
+    // AC coefficients whose code and magnitude bits fit in the next 9 bits:
+    // value << 16 | run << 8 | bits consumed (0 = not covered; EOB and ZRL
+    // are not covered). Derived from look_len/look_sym, so it decodes what
+    // decode_huff + getbits decode from the same bits.
+    int32_t fast_ac[512];
     bool present = false;
 };
 
@@ -121,6 +126,15 @@ bool build_huff(Huff &h, const uint8_t *counts, const uint8_t *symbols, int nsym
                 h.look_sym[e + k] = (uint8_t)sym;
             }
         }
+    }
+    for (int p = 0; p < 512; ++p) {
+        const int l = h.look_len[p >> 1], sym = h.look_sym[p >> 1];
+        const int r = sym >> 4, t = sym & 15;
+        h.fast_ac[p] = 0;
+        if (!l || !t || l + t > 9) continue;
+        const int v = (p >> (9 - l - t)) & ((1 << t) - 1);
+        const int val = (v < (1 << (t - 1))) ? v - (1 << t) + 1 : v;  // extend()
+        h.fast_ac[p] = (int32_t)((uint32_t)val << 16) | r << 8 | (l + t);
     }
     h.present = true;
     return true;
@@ -192,8 +206,22 @@ void decode_block(Jpeg &j, Comp &c, int16_t *out) {
         std::memset(out, 0, 64 * sizeof(int16_t));
         out[0] = (int16_t)c.pred;
     }
+    const Huff &ac = j.ac[c.ta];
     for (int k = 1; k < 64;) {
-        const int rs = decode_huff(j, j.ac[c.ta]);
+        fill(j);
+        if (const int32_t fa = ac.fast_ac[j.bitbuf >> 23]) {
+            k += (fa >> 8) & 15;
+            if (k > 63) {
+                j.err = ACMMP_ERR_IO;
+                return;
+            }
+            j.bitbuf <<= fa & 15;
+            j.bitcnt -= fa & 15;
+            if (out) out[kZigzag[k]] = (int16_t)(fa >> 16);
+            ++k;
+            continue;
+        }
+        const int rs = decode_huff(j, ac);
         const int r = rs >> 4, s = rs & 15;
         if (s == 0) {
             if (r != 15) break;  // EOB
@@ -1041,6 +1069,22 @@ int acmmp_internal_write_png(const char *path, int w, int h, int channels, const
     return write_png8(path, w, h, channels, px);
 }
 
+int acmmp_internal_read_image_bgr(const char *path, std::vector<uint8_t> &bgr, int &W, int &H) {
+    std::vector<uint8_t> buf;
+    if (!path || !read_file(path, buf)) return ACMMP_ERR_IO;
+    W = H = 0;
+    if (buf.size() >= 2 && buf[0] == 0xFF && buf[1] == 0xD8) return jpeg_decode(buf, false, W, H, nullptr, &bgr);
+    int C = 0, depth = 0;
+    std::vector<uint16_t> px;
+    const int rc = png_decode(buf, W, H, C, depth, &px);
+    if (rc) return rc;
+    if (depth != 8) return ACMMP_ERR_UNSUPPORTED;
+    bgr.resize((size_t)W * H * 3);
+    for (size_t i = 0; i < (size_t)W * H; ++i)
+        for (int k = 0; k < 3; ++k) bgr[3 * i + k] = (uint8_t)px[i * C + (C >= 3 ? k : 0)];
+    return ACMMP_OK;
+}
+
 extern "C" {
 
 int acmmp_image_size(const char *path, int *width, int *height) {
@@ -1068,24 +1112,9 @@ int acmmp_read_image_gray(const char *path, float *out, size_t capacity, int *wi
 
 int acmmp_read_image_bgr(const char *path, uint8_t *out, size_t capacity, int *width, int *height) {
     if (!width || !height) return ACMMP_ERR_ARG;
-    std::vector<uint8_t> buf;
-    if (!path || !read_file(path, buf)) return ACMMP_ERR_IO;
     int W = 0, H = 0;
     std::vector<uint8_t> bgr;
-    int rc;
-    if (buf.size() >= 2 && buf[0] == 0xFF && buf[1] == 0xD8) {
-        rc = jpeg_decode(buf, false, W, H, nullptr, &bgr);
-    } else {
-        int C = 0, depth = 0;
-        std::vector<uint16_t> px;
-        rc = png_decode(buf, W, H, C, depth, &px);
-        if (!rc) {
-            if (depth != 8) return ACMMP_ERR_UNSUPPORTED;
-            bgr.resize((size_t)W * H * 3);
-            for (size_t i = 0; i < (size_t)W * H; ++i)
-                for (int k = 0; k < 3; ++k) bgr[3 * i + k] = (uint8_t)px[i * C + (C >= 3 ? k : 0)];
-        }
-    }
+    const int rc = acmmp_internal_read_image_bgr(path, bgr, W, H);
     if (rc) return rc;
     *width = W;
     *height = H;
