@@ -356,10 +356,17 @@ struct Point {
 };
 
 // StoreColorPlyFileBinaryPointCloud. The 27-byte records (6 floats + r, g, b)
-// are formed in chunks of kPlyChunk points, each written at its own offset:
-// on the pool's workers when one is given (RunFusion's pool is idle by then),
-// else in order on the caller. Same bytes either way.
-constexpr size_t kPlyRec = 6 * sizeof(float) + 3, kPlyChunk = size_t(1) << 18;
+// are formed in chunks of 2^18 points, each written at its own offset: on
+// the pool's workers when one is given (RunFusion's pool is idle by then),
+// else in order on the caller. Same bytes either way. (ACMMP_PLY_CHUNK_POINTS
+// sets the chunk size, so tests reach the chunk boundaries on small clouds.)
+constexpr size_t kPlyRec = 6 * sizeof(float) + 3;
+
+size_t ply_chunk_points() {
+    const char *e = std::getenv("ACMMP_PLY_CHUNK_POINTS");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? (size_t)v : size_t(1) << 18;
+}
 
 int pwrite_all(int fd, const char *p, size_t n, off_t at) {
     while (n) {
@@ -380,9 +387,10 @@ int store_ply(const std::string &path, const std::vector<Point> &pc, Pool *pool 
                                  (int)pc.size());
     const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd < 0) return ffail(ACMMP_ERR_IO, "cannot write %s", path.c_str());
-    const int nchunks = (int)((pc.size() + kPlyChunk - 1) / kPlyChunk);
+    const size_t per = ply_chunk_points();
+    const int nchunks = (int)((pc.size() + per - 1) / per);
     auto chunk = [&](int c) -> int {
-        const size_t b = (size_t)c * kPlyChunk, e = std::min(pc.size(), b + kPlyChunk);
+        const size_t b = (size_t)c * per, e = std::min(pc.size(), b + per);
         std::vector<char> buf((e - b) * kPlyRec);
         char *o = buf.data();
         for (size_t k = b; k < e; ++k, o += kPlyRec) {

@@ -52,6 +52,28 @@ def test_fusion_matches_python_restatement(tmp_path):
     assert os.path.exists(os.path.join(d, "approved_pixels_cam_0.png"))
 
 
+def test_fusion_ply_chunks_write_the_same_bytes(tmp_path, monkeypatch):
+    """The PLY is formed and written in chunks on the fusion pool: with chunks
+    of 97 points (dozens of chunks, most records straddling nothing, every
+    boundary at an odd byte offset) the file is byte-identical to the
+    default single-chunk write, for RunFusion (pooled) and the prior-aware
+    fusion (sequential chunks)."""
+    d, out = _dense_with_maps(tmp_path)
+    path = os.path.join(out, "ACMMP_model.ply")
+    n = pipeline.run_fusion(d, out)
+    whole = open(path, "rb").read()
+    monkeypatch.setenv("ACMMP_PLY_CHUNK_POINTS", "97")
+    assert pipeline.run_fusion(d, out) == n and n > 20 * 97
+    assert open(path, "rb").read() == whole
+    prior = os.path.join(out, "ACMMP_prior_model.ply")
+    monkeypatch.delenv("ACMMP_PLY_CHUNK_POINTS")
+    pipeline.run_prior_aware_fusion(d, out, out)
+    whole = open(prior, "rb").read()
+    monkeypatch.setenv("ACMMP_PLY_CHUNK_POINTS", "97")
+    pipeline.run_prior_aware_fusion(d, out, out)
+    assert open(prior, "rb").read() == whole
+
+
 def test_fusion_thresholds_reduce_points(tmp_path):
     d, out = _dense_with_maps(tmp_path)
     n1 = pipeline.run_fusion(d, out, num_consistent_thresh=1)
