@@ -1407,7 +1407,11 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
                 }
             final_costs[i] = fc / weight_norm;
         }
-    } else if (ACMMP_GEOM_AHEAD & 1) {
+    } else if ((ACMMP_GEOM_AHEAD & 1) && NS <= 9) {
+        // (the 9-view bucket only: with 16-32 views the batch of fetches
+        // costs more than the latency it hides, geometric launch +0.2 / +0.6
+        // / +1.1 % at nsrc 16 / 20 / 21, profiles/r05_geom_ahead_ns.jsonl;
+        // those buckets take the per-view loop below)
         // views sampled by some lane of the wave (bit j; nsrc <= 32, so
         // padding slots j >= nsrc never appear)
         uint32_t wave_views = 0;

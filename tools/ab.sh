@@ -30,9 +30,8 @@ case "$mode" in
     for round in 1 2; do
       for spec in "$@"; do
         split_spec "$spec"
-        echo -n "{\"name\": \"$name\", \"round\": $round, \"t\": " >> gpurun_out/ab_pass.jsonl
-        env ACMMP_LIB=$lib $envv timeout -k 10 150 python3 tools/pass_times.py 2 >> gpurun_out/ab_pass.jsonl
-        rc=$?; echo "}" >> gpurun_out/ab_pass.jsonl
+        t=$(env ACMMP_LIB=$lib $envv timeout -k 10 150 python3 tools/pass_times.py 2)
+        rc=$?; echo "{\"name\": \"$name\", \"round\": $round, \"t\": ${t:-null}}" >> gpurun_out/ab_pass.jsonl
         echo "pass $name round $round rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done
     done

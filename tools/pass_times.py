@@ -4,6 +4,8 @@ geometric pass with the geometric cost's depth fetch counted: the bench's
 launch_ms is their mean.
 
 usage: python tools/pass_times.py [reps] > gpurun_out/pass_times.json
+(PASS_NSRC=<n> in the environment: n source views instead of cfg2's 9, so the
+NS 16 / 20 / 32 kernel buckets can be timed.)
 """
 import json
 import os
@@ -16,7 +18,8 @@ from acmmp_amd import default_params, scene  # noqa: E402
 from acmmp_amd.resident import EnginePool, geometric_view, photometric_view  # noqa: E402
 
 REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-W, H, NSRC, ITERS = 1600, 1200, 9, 8
+W, H, ITERS = 1600, 1200, 8
+NSRC = int(os.environ.get("PASS_NSRC", "9"))
 dev = torch.device("cuda", 0)
 
 
