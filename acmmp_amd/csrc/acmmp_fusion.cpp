@@ -580,12 +580,32 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
                 m16.resize((size_t)mw * mh * mc);
                 rc = acmmp_read_png(mpath.c_str(), m16.data(), m16.size(), &mw, &mh, &mc, &bd);
             }
-            if (rc || bd != 8) return ffail(ACMMP_ERR_IO, "Couldn't find mask image %s", mpath.c_str());
-            std::vector<uint8_t> m8((size_t)mw * mh), mr;
-            for (size_t k = 0; k < m8.size(); ++k) m8[k] = (uint8_t)m16[k * mc];
-            resize_u8(m8, mw, mh, 1, mr, w, h);
-            for (size_t k = 0; k < mr.size(); ++k)
-                if (mr[k] < 128) masks[i].set(k);
+            if (rc) return ffail(ACMMP_ERR_IO, "Couldn't find mask image %s", mpath.c_str());
+            // cv::imread(path, -1) keeps the file's depth and channels (colour
+            // as B, G, R[, A], as acmmp_read_png returns them too);
+            // `(temp_mask < 128) / 255` keeps the channels,
+            // and the walk reads and writes the mask with at<uchar>(r, c):
+            // byte c of row r. For a 1-channel mask that is pixel (r, c); for
+            // a colour one it is channel c % C of pixel c / C, reproduced here.
+            // (2-channel gray+alpha masks use the gray value: unpinned.)
+            const bool same = mw == w && mh == h;
+            if (bd != 8 && !same)
+                return ffail(ACMMP_ERR_UNSUPPORTED, "16-bit mask %s needs resizing", mpath.c_str());
+            const int C = mc == 2 ? 1 : mc;
+            std::vector<uint16_t> px((size_t)mw * mh * C);
+            for (size_t k = 0; k < (size_t)mw * mh; ++k)
+                for (int ch = 0; ch < C; ++ch) px[k * C + ch] = m16[k * mc + ch];
+            std::vector<uint16_t> mr;
+            if (same) {
+                mr.swap(px);
+            } else {
+                std::vector<uint8_t> m8(px.begin(), px.end()), r8;
+                resize_u8(m8, mw, mh, C, r8, w, h);
+                mr.assign(r8.begin(), r8.end());
+            }
+            for (int r = 0; r < h; ++r)
+                for (int c = 0; c < w; ++c)
+                    if (mr[(size_t)r * w * C + c] < 128) masks[i].set((size_t)r * w + c);
         }
         return (int)ACMMP_OK;
     });

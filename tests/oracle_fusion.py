@@ -51,7 +51,22 @@ def _angle(a, b):
     return f32(0.0) if ang != ang else ang
 
 
-def run_fusion(dense, out, geom=True, consistency_scalar=0.3, con_num_thresh=1):
+def _initial_mask(dense, mask_folder, ref_id, shape):
+    """:881-905: cv::imread(mask, -1) (the file's depth and channels, colour as
+    B, G, R[, A]), mask = (mask < 128) / 255, then read and written with
+    at<uchar>(r, c), i.e. byte c of row r of the (possibly multi-channel)
+    mask. Masks of the depth map's size only (cv::resize is then the identity)."""
+    from PIL import Image
+    a = np.asarray(Image.open(os.path.join(dense, mask_folder, "%08d.png" % ref_id)))
+    if a.ndim == 3:
+        a = np.concatenate([a[..., 2::-1], a[..., 3:]], -1)  # RGB[A] -> BGR[A]
+    H, W = shape
+    assert a.shape[:2] == (H, W)
+    rows = a.reshape(H, -1)
+    return (rows[:, :W] < 128).astype(np.uint8)
+
+
+def run_fusion(dense, out, geom=True, consistency_scalar=0.3, con_num_thresh=1, mask_folder=None):
     from PIL import Image
     problems = aio.read_pair(os.path.join(dense, "pair.txt"))
     index = {p.ref_image_id: i for i, p in enumerate(problems)}
@@ -63,7 +78,8 @@ def run_fusion(dense, out, geom=True, consistency_scalar=0.3, con_num_thresh=1):
         rf = aio.result_folder(out, p.ref_image_id)
         depths.append(aio.read_dmb(os.path.join(rf, "depths_geom.dmb" if geom else "depths.dmb")))
         normals.append(aio.read_dmb(os.path.join(rf, "normals.dmb")))
-        masks.append(np.zeros(depths[-1].shape, np.uint8))
+        masks.append(np.zeros(depths[-1].shape, np.uint8) if mask_folder is None else
+                     _initial_mask(dense, mask_folder, p.ref_image_id, depths[-1].shape))
     cloud = []
     for i, p in enumerate(problems):
         H, W = depths[i].shape

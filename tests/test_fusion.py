@@ -5,6 +5,7 @@ binary PLY must match point for point, bit-exactly."""
 import os
 
 import numpy as np
+import pytest
 
 from acmmp_amd import io as aio
 from acmmp_amd import pipeline, scene
@@ -72,6 +73,35 @@ def test_fusion_ply_chunks_write_the_same_bytes(tmp_path, monkeypatch):
     monkeypatch.setenv("ACMMP_PLY_CHUNK_POINTS", "97")
     pipeline.run_prior_aware_fusion(d, out, out)
     assert open(prior, "rb").read() == whole
+
+
+@pytest.mark.parametrize("kind", ["gray8", "bgr8", "gray16"])
+def test_fusion_with_masks_matches_restatement(tmp_path, kind):
+    """RunFusion's mask folder (src/acmmp_definitions.cpp:881-905): masked
+    pixels are skipped as references and as sources from the start. The mask
+    is read as cv::imread(-1) reads it and indexed as the reference indexes
+    it (at<uchar>(r, c): byte c of row r, which for a colour mask is channel
+    c % 3 of pixel c / 3); 8-bit gray, 8-bit colour and 16-bit gray PNGs."""
+    from PIL import Image
+    d, out = _dense_with_maps(tmp_path)
+    os.makedirs(os.path.join(d, "masks"))
+    rng = np.random.default_rng(5)
+    for i in range(4):
+        H, W = 54, 72
+        if kind == "bgr8":
+            m = rng.integers(60, 256, (H, W, 3)).astype(np.uint8)
+            img = Image.fromarray(m, "RGB")
+        elif kind == "gray16":
+            img = Image.fromarray(rng.integers(40, 400, (H, W)).astype(np.uint16))
+        else:
+            img = Image.fromarray(rng.integers(70, 256, (H, W)).astype(np.uint8), "L")
+        img.save(os.path.join(d, "masks", "%08d.png" % i))
+    n = pipeline.run_fusion(d, out, mask_folder="masks")
+    ply = read_ply(os.path.join(out, "ACMMP_model.ply"))
+    ref = run_fusion(d, out, mask_folder="masks")
+    free = run_fusion(d, out)
+    assert 100 < n < len(free)
+    _compare_cloud(ply, ref)
 
 
 def test_fusion_thresholds_reduce_points(tmp_path):
