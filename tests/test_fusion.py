@@ -104,6 +104,24 @@ def test_fusion_with_masks_matches_restatement(tmp_path, kind):
     _compare_cloud(ply, ref)
 
 
+def test_fusion_photometric_maps_and_thresholds_match_restatement(tmp_path):
+    """geom_consistency = false reads depths.dmb (:867-870), and the two
+    thresholds (:1007) change which pixels are approved; both against the
+    restatement, PLY point for point."""
+    d, out = _dense_with_maps(tmp_path)
+    rng = np.random.default_rng(3)
+    for i in range(4):
+        rf = aio.result_folder(out, i)
+        dep = aio.read_dmb(os.path.join(rf, "depths_geom.dmb"))
+        dep = np.where(rng.random(dep.shape) < 0.2, dep * np.float32(1.004), dep).astype(np.float32)
+        aio.write_dmb(os.path.join(rf, "depths.dmb"), dep)
+    for geom, scalar, thresh in ((False, 0.3, 1), (True, 0.4, 2), (False, 0.35, 2)):
+        n = pipeline.run_fusion(d, out, geom_consistency=geom, consistency_scalar=scalar, num_consistent_thresh=thresh)
+        ref = run_fusion(d, out, geom=geom, consistency_scalar=scalar, con_num_thresh=thresh)
+        assert n > 1000, (geom, scalar, thresh, n)
+        _compare_cloud(read_ply(os.path.join(out, "ACMMP_model.ply")), ref)
+
+
 def test_fusion_thresholds_reduce_points(tmp_path):
     d, out = _dense_with_maps(tmp_path)
     n1 = pipeline.run_fusion(d, out, num_consistent_thresh=1)
