@@ -106,6 +106,23 @@ def test_t2_init_and_one_sweep(small_scene, iters):
     assert_bit_exact(sv, ref["selected_views"], "selected views")
 
 
+@pytest.mark.parametrize("sigma_spatial,sigma_color,top_k", [(3.5, 7.0, 2), (6.0, 1.5, 6)])
+def test_t3_nondefault_patch_parameters(small_scene, sigma_spatial, sigma_color, top_k):
+    """PatchMatchParams' bilateral sigmas (the patch weights, src/ACMMP.cu:
+    360-380) and top_k (the initial cost's best-k mean and selected views,
+    :434-471) at values other than the defaults: GPU and oracle bit-exact."""
+    cams, imgs = small_scene.problem(0, 9)
+    p = _params(2, sigma_spatial=sigma_spatial, sigma_color=sigma_color, top_k=top_k)
+    prm, pl, co, sv = _gpu_run(p, cams, imgs)
+    assert (prm.sigma_spatial, prm.sigma_color, prm.top_k) == (sigma_spatial, sigma_color, top_k)
+    ref = oracle.run_patchmatch(prm, cams, imgs)
+    assert_bit_exact(pl, ref["planes"], "planes")
+    assert_bit_exact(co, ref["costs"], "costs")
+    assert_bit_exact(sv, ref["selected_views"], "selected views")
+    _, pl_default, _, _ = _gpu_run(_params(2), cams, imgs)
+    assert not np.array_equal(pl, pl_default)  # the parameters reach the kernels
+
+
 def test_t3_photometric_cfg1_shape():
     """cfg1: 5 views at 400x300, 3 iterations, photometric (the reference's
     CPU-sized configuration)."""
