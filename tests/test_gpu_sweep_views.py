@@ -59,7 +59,7 @@ def test_sweep_parity_across_view_counts(nsrc, W, H):
         assert counts.max() >= 2
 
 
-@pytest.mark.parametrize("nsrc", [12, 20])
+@pytest.mark.parametrize("nsrc", [12, 20, 25])
 def test_geometric_sweep_many_views(nsrc):
     """A photometric pass, then a geometric pass from its state that reads
     the source views' ground-truth depth maps (geom_cost on every sampled
