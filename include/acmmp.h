@@ -456,7 +456,11 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
  * of `fusion_folder` with this run's (`output_folder`) seeded maps as priors,
  * per pixel choosing the hypothesis with more consistent views
  * (single_match_penalty for one-sided support), into
- * <output>/ACMMP_prior_model.ply. Host code, literal. */
+ * <output>/ACMMP_prior_model.ply. Host code, literal. The reference's
+ * mask_folder argument (:579, :657-666) is not taken: its mask is
+ * `Mat_<Vec3b>(imread(path, -1)) < 128`, i.e. 0 / 255, and the walk skips a
+ * pixel only where the mask byte == 1, which only its own approvals write, so
+ * a readable mask file changes nothing (an unreadable one crashes it). */
 int acmmp_run_prior_aware_fusion(const char *dense_folder, const char *output_folder, const char *fusion_folder,
                                  const acmmp_problem *problems, int count, int geom_consistency,
                                  float consistency_scalar, int num_consistent_thresh, int single_match_penalty,
