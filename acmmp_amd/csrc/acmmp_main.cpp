@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/acmmp.h"
@@ -48,7 +50,9 @@ void usage() {
         "                           sharded per pass, depth maps all-gathered (Jacobi order); rank 0 fuses\n"
         "  --exchange rccl|tcp      view-parallel all-gather: RCCL or TCP via the rendezvous (default:\n"
         "                           RCCL at world > 1, a device copy at world 1)\n"
-        "  --concurrent_views N     view-parallel: engines (HIP streams) per GPU (2)\n"
+        "  --concurrent_views N     engines (HIP streams) per GPU (2): views in flight in the view-parallel\n"
+        "                           driver, and in the sequential order's passes without geometric\n"
+        "                           consistency (their views are independent; 1 = one at a time)\n"
         "  --no_split_tail          view-parallel: compute the V mod world tail views whole instead of\n"
         "                           in row bands over all ranks\n");
 }
@@ -177,6 +181,7 @@ int main(int argc, char **argv) {
     opt.write_triangulation = triangulation ? 1 : 0;
     opt.verbose = quiet ? 0 : 1;
     unsigned pass = 0;
+    std::string pass_error;  // the first failing view's message (set by run_pass)
     auto run_pass = [&](bool geom, bool planar, bool hier, bool multi, bool seeded = false) -> bool {
         opt.seeded = seeded;
         opt.geom_consistency = geom;
@@ -184,13 +189,45 @@ int main(int argc, char **argv) {
         opt.hierarchy = hier;
         opt.multi_geometry = multi;
         opt.seed_hi = pass++;
-        for (int i = 0; i < num_images; ++i) {
-            opt.seed_lo = seed + (unsigned)problems[(size_t)i].ref_image_id;
-            if (acmmp_process_problem(dense_folder.c_str(), output_folder.c_str(), problems.data(), num_images, i,
-                                      &opt))
+        // A pass without geometric consistency reads no map written in the
+        // same pass (each view: its images, its own earlier maps, its own
+        // prior), so its views are independent and `concurrent_views` of them
+        // run at once, each with its own engine and HIP stream (one view's
+        // host I/O and prior construction overlap another's kernels); the
+        // outputs are those of the one-at-a-time loop. A geometric pass reads
+        // the maps its earlier views have just written (the reference's
+        // order, src/main_ACMMP.cpp:159-172) and runs one view at a time.
+        const int lanes = geom ? 1 : std::max(1, std::min(concurrent_views, num_images));
+        std::vector<int> rc((size_t)num_images, 0);
+        std::vector<std::string> msg((size_t)num_images);
+        std::atomic<int> next{0};
+        std::atomic<bool> failed{false};
+        auto worker = [&] {
+            for (int i; !failed.load() && (i = next.fetch_add(1)) < num_images;) {
+                acmmp_pass_options o = opt;
+                o.seed_lo = seed + (unsigned)problems[(size_t)i].ref_image_id;
+                rc[(size_t)i] = acmmp_process_problem(dense_folder.c_str(), output_folder.c_str(), problems.data(),
+                                                      num_images, i, &o);
+                if (rc[(size_t)i]) {
+                    msg[(size_t)i] = acmmp_pipeline_last_error();
+                    failed = true;
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < lanes; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto &t : pool) t.join();
+        for (int i = 0; i < num_images; ++i)
+            if (rc[(size_t)i]) {
+                pass_error = msg[(size_t)i];
                 return false;
-        }
+            }
         return true;
+    };
+    auto die_pass = [&](const char *what) {
+        std::fprintf(stderr, "acmmp_main: %s: %s\n", what, pass_error.c_str());
+        return 1;
     };
 
     const int geom_iterations = 2;
@@ -228,17 +265,17 @@ int main(int argc, char **argv) {
         }
         if (flag == 0) {
             flag = 1;
-            if (!run_pass(false, true, false, false, prior)) return die("ProcessProblem");
+            if (!run_pass(false, true, false, false, prior)) return die_pass("ProcessProblem");
         } else {
             if (!quiet) std::printf("Starting JBU\n");
             for (auto &p : problems)
                 if (acmmp_joint_bilateral_upsampling(dense_folder.c_str(), output_folder.c_str(), &p,
                                                      p.cur_image_size, device))
                     return die("JointBilateralUpsampling");
-            if (!run_pass(false, true, true, false)) return die("ProcessProblem");
+            if (!run_pass(false, true, true, false)) return die_pass("ProcessProblem");
         }
         for (int g = 0; g < geom_iterations; ++g)
-            if (!run_pass(true, false, false, g > 0)) return die("ProcessProblem");
+            if (!run_pass(true, false, false, g > 0)) return die_pass("ProcessProblem");
         max_num_downscale--;
     }
     if (!fusion) return 0;

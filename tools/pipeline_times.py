@@ -16,7 +16,8 @@ Synthetic, seeded scene rendered on the GPU and written as 8-bit JPEGs (a
 COLMAP-converted dense folder); wall times include JPEG decode and .dmb I/O,
 as the reference's do. Iterations: the driver's default (the reference's).
 usage: python tools/pipeline_times.py [views] [width] [height] [nsrc] [steps] > gpurun_out/pipeline.jsonl
-  steps: comma list of distributed,cli_vp,cli,fusion,fusion_dist (default distributed,cli,fusion;
+  steps: comma list of distributed,cli_vp,cli,cli_serial,fusion,fusion_dist (default distributed,cli,fusion;
+         cli_serial also runs the CLI with --concurrent_views 1 and compares the two's maps;
          fusion fuses the CLI's maps, fusion_dist the distributed driver's, once per library in
          ACMMP_FUSION_LIBS (comma list, default the product) in a subprocess each)
 
@@ -143,9 +144,21 @@ def main():
         return
 
     cli = os.path.join(ROOT, "acmmp_amd", "lib", "acmmp_main")
+    if "cli_serial" in STEPS:  # one view at a time in every pass (--concurrent_views 1)
+        t0 = time.perf_counter()
+        subprocess.run([cli, dense, "--output_dir", "/ACMMP_serial", "--no_fusion", "--concurrent_views", "1"],
+                       stdout=sys.stderr, check=True)
+        emit(step="cli_serial", order="sequential", concurrent_views=1, s=round(time.perf_counter() - t0, 2))
     t0 = time.perf_counter()
     subprocess.run([cli, dense, "--output_dir", "/ACMMP", "--no_fusion"], stdout=sys.stderr, check=True)
-    emit(step="cli", order="sequential", s=round(time.perf_counter() - t0, 2))
+    emit(step="cli", order="sequential", concurrent_views=2, s=round(time.perf_counter() - t0, 2))
+    if "cli_serial" in STEPS:  # the non-geometric passes' views in flight change no output byte
+        diff = [f for f in sorted(os.listdir(dense + "/ACMMP_serial")) for m in ("depths_geom.dmb", "normals.dmb",
+                                                                                   "costs.dmb")
+                if open(os.path.join(dense, "ACMMP_serial", f, m), "rb").read()
+                != open(os.path.join(dense, "ACMMP", f, m), "rb").read()]
+        emit(step="cli_vs_cli_serial", identical=not diff, differing=diff[:5])
+        shutil.rmtree(dense + "/ACMMP_serial", ignore_errors=True)
 
     t0 = time.perf_counter()
     n = pipeline.run_fusion(dense, dense + "/ACMMP")
