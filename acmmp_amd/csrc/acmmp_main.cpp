@@ -51,8 +51,8 @@ void usage() {
         "  --exchange rccl|tcp      view-parallel all-gather: RCCL or TCP via the rendezvous (default:\n"
         "                           RCCL at world > 1, a device copy at world 1)\n"
         "  --concurrent_views N     engines (HIP streams) per GPU (2): views in flight in the view-parallel\n"
-        "                           driver, and in the sequential order's passes without geometric\n"
-        "                           consistency (their views are independent; 1 = one at a time)\n"
+        "                           driver, and in the sequential order's passes whose views are\n"
+        "                           independent (all but multi-geometry; 1 = one at a time)\n"
         "  --no_split_tail          view-parallel: compute the V mod world tail views whole instead of\n"
         "                           in row bands over all ranks\n");
 }
@@ -189,15 +189,18 @@ int main(int argc, char **argv) {
         opt.hierarchy = hier;
         opt.multi_geometry = multi;
         opt.seed_hi = pass++;
-        // A pass without geometric consistency reads no map written in the
-        // same pass (each view: its images, its own earlier maps, its own
-        // prior), so its views are independent and `concurrent_views` of them
-        // run at once, each with its own engine and HIP stream (one view's
-        // host I/O and prior construction overlap another's kernels); the
-        // outputs are those of the one-at-a-time loop. A geometric pass reads
-        // the maps its earlier views have just written (the reference's
-        // order, src/main_ACMMP.cpp:159-172) and runs one view at a time.
-        const int lanes = geom ? 1 : std::max(1, std::min(concurrent_views, num_images));
+        // A view of a pass reads its images, its own maps of earlier passes
+        // (and its own prior), and in a geometric pass its sources' depth
+        // maps: depths.dmb in the first geometric pass, depths_geom.dmb in
+        // the multi-geometry ones (src/ACMMP.cpp:608-635, 707-742); it writes
+        // only its own folder. Only a multi-geometry pass reads files written
+        // in the same pass (its earlier views' depths_geom.dmb: the
+        // reference's order, src/main_ACMMP.cpp:159-172), so it runs one view
+        // at a time; in every other pass the views are independent and
+        // `concurrent_views` of them run at once, each with its own engine and
+        // HIP stream (one view's host I/O and prior construction overlap
+        // another's kernels), with the outputs of the one-at-a-time loop.
+        const int lanes = (geom && multi) ? 1 : std::max(1, std::min(concurrent_views, num_images));
         std::vector<int> rc((size_t)num_images, 0);
         std::vector<std::string> msg((size_t)num_images);
         std::atomic<int> next{0};
