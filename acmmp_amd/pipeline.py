@@ -120,9 +120,15 @@ def scale_step(problems: list) -> None:
 
 def run_sequential(dense_folder: str, output_dir: str | None = None, device: int = 0, max_iterations: int = 0,
                    seed: int = 1234, write_triangulation: bool = True, geom_iterations: int = 2,
-                   verbose: bool = False, prior: bool = False) -> str:
+                   verbose: bool = False, prior: bool = False, concurrent_views: int = 2) -> str:
     """main_ACMMP's multi-scale loop without fusion; returns the output folder.
-    prior=True is the -p flag: seeded first pass, default folder /ACMMP_PRIOR."""
+    prior=True is the -p flag: seeded first pass, default folder /ACMMP_PRIOR.
+
+    The views of a pass that reads no file written in the same pass (every
+    pass but the multi-geometry ones: a first geometric pass reads its
+    sources' depths.dmb, which it does not write) run `concurrent_views` at a
+    time, each call with its own engine and stream (the C-ABI call releases
+    the GIL); the outputs are those of one view at a time, as in acmmp_main."""
     problems = generate_sample_list(dense_folder)
     max_num_downscale = compute_multiscale_settings(dense_folder, problems)
     if prior and not priors_available(dense_folder, len(problems)):
@@ -134,10 +140,19 @@ def run_sequential(dense_folder: str, output_dir: str | None = None, device: int
     state = {"pass": 0}
 
     def run_pass(geom, planar, hier, multi, seeded=False):
-        for i, p in enumerate(problems):
-            opt = pass_options(geom, planar, hier, multi, device, max_iterations, seed + p.ref_image_id,
-                               state["pass"], write_triangulation, verbose, seeded)
-            process_problem(dense_folder, output_folder, problems, i, opt)
+        opts = [pass_options(geom, planar, hier, multi, device, max_iterations, seed + p.ref_image_id,
+                             state["pass"], write_triangulation, verbose, seeded) for p in problems]
+        lanes = 1 if (geom and multi) else max(1, min(concurrent_views, len(problems)))
+        if lanes == 1:
+            for i in range(len(problems)):
+                process_problem(dense_folder, output_folder, problems, i, opts[i])
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(lanes) as ex:
+                futs = [ex.submit(process_problem, dense_folder, output_folder, problems, i, opts[i])
+                        for i in range(len(problems))]
+                for f in futs:  # the first failing view in order, as the loop reports it
+                    f.result()
         state["pass"] += 1
 
     first = True
