@@ -113,16 +113,34 @@ inline int set_err(acmmp_ctx *ctx, int code, const char *fmt, ...) {
                            hipGetErrorString(e_), __FILE__, __LINE__);                       \
     } while (0)
 
+// Device blocks (acmmp_engine.hip). hipFree synchronises the whole device —
+// with two engines in flight it waits for the other one's kernels — and
+// costs about a millisecond per block, so blocks freed where their engine's
+// stream has just been synchronised (dfree_synced; every free of
+// acmmp_destroy) go to a per-(device, size) cache that later allocations of
+// the same size take from. ACMMP_DEVICE_POOL_MB caps it (default 8192; 0
+// turns it off). Any other free goes to hipFree, as before.
+hipError_t dev_alloc(void **p, size_t bytes);
+void dev_free(void *p, bool synced);
+extern thread_local bool g_frees_synced;  // set by acmmp_destroy after its stream sync
+
 template <typename T>
 inline void dfree(T *&p) {
-    if (p) (void)hipFree((void *)p);
+    if (p) dev_free((void *)p, g_frees_synced);
+    p = nullptr;
+}
+
+// for a block no queued work can still touch (its stream just synchronised)
+template <typename T>
+inline void dfree_synced(T *&p) {
+    if (p) dev_free((void *)p, true);
     p = nullptr;
 }
 
 template <typename T>
 inline hipError_t dalloc(T *&p, size_t count) {
     dfree(p);
-    return hipMalloc((void **)&p, count * sizeof(T) > 0 ? count * sizeof(T) : 4);
+    return dev_alloc((void **)&p, count * sizeof(T) > 0 ? count * sizeof(T) : 4);
 }
 
 inline int pitch_of(int w) { return (w + 63) / 64 * 64; }

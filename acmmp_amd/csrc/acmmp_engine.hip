@@ -12,11 +12,106 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "acmmp_ctx.h"
 
+
+thread_local bool acmmp::g_frees_synced = false;
+
+namespace {
+
+// the device-block cache of dev_alloc / dev_free (acmmp_ctx.h)
+struct DevPool {
+    std::mutex mu;
+    std::unordered_map<void *, size_t> size_of;                    // every live dev_alloc block
+    std::map<std::pair<int, size_t>, std::vector<void *>> free_;  // (device, bytes) -> cached blocks
+    size_t cached = 0, cap = 0;
+    DevPool() {
+        const char *e = std::getenv("ACMMP_DEVICE_POOL_MB");
+        cap = (size_t)(e ? std::atoll(e) : 8192) << 20;
+    }
+};
+DevPool &devpool() {
+    static DevPool *p = new DevPool();  // never destroyed: blocks outlive static destruction order
+    return *p;
+}
+
+// the engines' pinned KViews staging blocks, cached the same way (hipHostFree
+// synchronises the device too); freed only by acmmp_destroy, after its sync
+std::mutex g_pinned_mu;
+std::vector<KViews *> g_pinned_kv;
+
+hipError_t pinned_kv_alloc(KViews **p) {
+    {
+        std::lock_guard<std::mutex> g(g_pinned_mu);
+        if (devpool().cap && !g_pinned_kv.empty()) {
+            *p = g_pinned_kv.back();
+            g_pinned_kv.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipHostMalloc((void **)p, sizeof(KViews), hipHostMallocDefault);
+}
+
+void pinned_kv_free(KViews *p) {
+    {
+        std::lock_guard<std::mutex> g(g_pinned_mu);
+        if (devpool().cap && g_pinned_kv.size() < 64) {
+            g_pinned_kv.push_back(p);
+            return;
+        }
+    }
+    (void)hipHostFree(p);
+}
+
+}  // namespace
+
+hipError_t acmmp::dev_alloc(void **p, size_t bytes) {
+    DevPool &pool = devpool();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> g(pool.mu);
+        auto it = pool.free_.find({dev, bytes});
+        if (it != pool.free_.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            pool.cached -= bytes;
+            pool.size_of[*p] = bytes;
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> g(pool.mu);
+        pool.size_of[*p] = bytes;
+    }
+    return e;
+}
+
+void acmmp::dev_free(void *p, bool synced) {
+    DevPool &pool = devpool();
+    {
+        std::lock_guard<std::mutex> g(pool.mu);
+        auto it = pool.size_of.find(p);
+        const size_t bytes = it == pool.size_of.end() ? 0 : it->second;
+        if (it != pool.size_of.end()) pool.size_of.erase(it);
+        if (synced && bytes && pool.cached + bytes <= pool.cap) {
+            hipPointerAttribute_t a;
+            int dev = 0;
+            if (hipPointerGetAttributes(&a, p) == hipSuccess) dev = a.device;
+            pool.free_[{dev, bytes}].push_back(p);
+            pool.cached += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
 
 namespace {
 
@@ -134,8 +229,8 @@ int kv_upload(acmmp_ctx *ctx) {
     const int k = ctx->kv_slot;
     ctx->kv_slot = (k + 1) % acmmp_ctx::kSlots;
     if (!ctx->d_kv_ring[k]) {
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_kv_ring[k], sizeof(KViews)));
-        HIP_TRY(ctx, hipHostMalloc((void **)&ctx->h_kv_ring[k], sizeof(KViews), hipHostMallocDefault));
+        HIP_TRY(ctx, dalloc(ctx->d_kv_ring[k], 1));
+        HIP_TRY(ctx, pinned_kv_alloc(&ctx->h_kv_ring[k]));
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->kv_ev[k], hipEventDisableTiming));
     }
     if (ctx->kv_used[k]) HIP_TRY(ctx, hipEventSynchronize(ctx->kv_ev[k]));
@@ -454,13 +549,16 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // nothing queued can touch the engine's blocks now: they go to the cache
+    g_frees_synced = true;
     free_images(ctx);
     free_state(ctx);
     for (auto &p : ctx->pad) dfree(p);
     dfree(ctx->d_not_u8);
+    for (int k = 0; k < acmmp_ctx::kSlots; ++k) dfree(ctx->d_kv_ring[k]);
+    g_frees_synced = false;
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
-        dfree(ctx->d_kv_ring[k]);
-        if (ctx->h_kv_ring[k]) (void)hipHostFree(ctx->h_kv_ring[k]);
+        if (ctx->h_kv_ring[k]) pinned_kv_free(ctx->h_kv_ring[k]);
         if (ctx->kv_ev[k]) (void)hipEventDestroy(ctx->kv_ev[k]);
     }
     if (ctx->events_made)

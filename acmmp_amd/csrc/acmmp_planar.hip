@@ -226,7 +226,8 @@ int acmmp_get_support_points(acmmp_ctx *ctx, int32_t *xy, int capacity, int *cou
     if (e == hipSuccess)
         e = hipMemcpyAsync(h.data(), d_out, nblocks * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    dfree(d_out);
+    if (e == hipSuccess) dfree_synced(d_out);
+    else dfree(d_out);
     HIP_TRY(ctx, e);
     int n = 0;
     for (int b = 0; b < nblocks; ++b) {
@@ -291,9 +292,9 @@ int acmmp_build_planar_prior(acmmp_ctx *ctx, const int32_t *tris, int ntris, flo
         HIP_TRY(ctx, hipMemcpyAsync(out_planes4, d_planes, (size_t)nt * sizeof(float4), hipMemcpyDeviceToHost, s));
     if (out_mask) HIP_TRY(ctx, hipMemcpyAsync(out_mask, ctx->d_mask, P * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
-    dfree(d_tris);
-    dfree(d_planes);
-    dfree(d_overflow);
+    dfree_synced(d_tris);
+    dfree_synced(d_planes);
+    dfree_synced(d_overflow);
     if (overflow) return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "%d triangles longer than %d px", overflow, kMaxSeq);
     ctx->have_prior = true;
     return ACMMP_OK;
