@@ -191,23 +191,29 @@ void draw_line(std::vector<uint8_t> &rgb, int w, int h, acmmp::Point a, acmmp::P
     }
 }
 
-int write_triangulation(acmmp::ACMMP &acmmp, const std::string &path) {
+// The triangulation picture of ProcessProblem (:301-331): the support points'
+// Delaunay triangles drawn on the reference image. Returns the picture and
+// the triangles (x1 y1 x2 y2 x3 y3 each), which the planar prior is built
+// from too, as the reference builds both from one triangulation.
+void triangulation_picture(acmmp::ACMMP &acmmp, std::vector<uint8_t> &rgb, std::vector<int32_t> &flat) {
     const int W = acmmp.GetReferenceImageWidth(), H = acmmp.GetReferenceImageHeight();
     const acmmp::Image ref = acmmp.GetReferenceImage();
     std::vector<acmmp::Point> pts;
     acmmp.GetSupportPoints(pts);
     const auto tris = acmmp.DelaunayTriangulation(W, H, pts);
-    std::vector<uint8_t> rgb((size_t)W * H * 3);
+    rgb.assign((size_t)W * H * 3, 0);
     for (size_t i = 0; i < (size_t)W * H; ++i) {
         const float v = std::nearbyint(std::min(255.0f, std::max(0.0f, ref.data[i])));
         rgb[3 * i] = rgb[3 * i + 1] = rgb[3 * i + 2] = (uint8_t)v;
     }
+    flat.clear();
+    flat.reserve(tris.size() * 6);
     for (const auto &t : tris) {
         draw_line(rgb, W, H, t.pt1, t.pt2);
         draw_line(rgb, W, H, t.pt1, t.pt3);
         draw_line(rgb, W, H, t.pt2, t.pt3);
+        flat.insert(flat.end(), {t.pt1.x, t.pt1.y, t.pt2.x, t.pt2.y, t.pt3.x, t.pt3.y});
     }
-    return write_png8(path, W, H, 3, rgb.data());
 }
 
 // Runs fn(0..n-1) on acmmp_host_threads() threads. Returns the status of the lowest
@@ -590,12 +596,32 @@ int acmmp_process_problem(const char *dense_folder, const char *output_folder, c
         if (opt->planar_prior) {  // :301-379
             if (opt->verbose) std::printf("Run Planar Prior Assisted PatchMatch MVS ...\n");
             if (opt->write_triangulation) {
-                const int rc = write_triangulation(acmmp, folder + "/triangulation.png");
-                if (rc) return rc;
+                // one triangulation for the picture and the prior; the PNG is
+                // encoded on a helper thread while the second PatchMatch runs
+                std::vector<uint8_t> rgb;
+                std::vector<int32_t> tris;
+                triangulation_picture(acmmp, rgb, tris);
+                const int rc = acmmp_build_planar_prior(acmmp.handle(), tris.data(), (int)(tris.size() / 6), nullptr,
+                                                        nullptr);
+                if (rc) return fail(rc, "%s", acmmp_last_error(acmmp.handle()));
+                acmmp.SetPlanarPriorParams();
+                clk.mark("planar_prior");
+                const std::string png_path = folder + "/triangulation.png";
+                int png_rc = ACMMP_OK;  // (the error message is set on this thread, below)
+                std::thread png([&] { png_rc = acmmp_internal_write_png(png_path.c_str(), width, height, 3, rgb.data()); });
+                try {
+                    acmmp.RunPatchMatch();
+                } catch (...) {
+                    png.join();
+                    throw;
+                }
+                png.join();
+                if (png_rc) return fail(ACMMP_ERR_IO, "cannot write %s", png_path.c_str());
+            } else {
+                acmmp.PreparePlanarPrior();  // support points, Delaunay, prior planes; SetPlanarPriorParams
+                clk.mark("planar_prior");
+                acmmp.RunPatchMatch();
             }
-            acmmp.PreparePlanarPrior();  // support points, Delaunay, prior planes; SetPlanarPriorParams
-            clk.mark("planar_prior");
-            acmmp.RunPatchMatch();
             clk.mark("patchmatch2");
         }
         const auto &planes = acmmp.GetPlaneHypotheses();
