@@ -181,7 +181,36 @@ int main(int argc, char **argv) {
     opt.write_triangulation = triangulation ? 1 : 0;
     opt.verbose = quiet ? 0 : 1;
     unsigned pass = 0;
-    std::string pass_error;  // the first failing view's message (set by run_pass)
+    std::string pass_error;  // the first failing view's message (set by for_views)
+    // fn(0..num_images-1), `lanes` views at a time; false (and pass_error =
+    // the lowest failing view's message, what the one-at-a-time loop reports)
+    // if any fails
+    auto for_views = [&](int lanes, auto fn) -> bool {
+        lanes = std::max(1, std::min(lanes, num_images));
+        std::vector<int> rc((size_t)num_images, 0);
+        std::vector<std::string> msg((size_t)num_images);
+        std::atomic<int> next{0};
+        std::atomic<bool> failed{false};
+        auto worker = [&] {
+            for (int i; !failed.load() && (i = next.fetch_add(1)) < num_images;) {
+                rc[(size_t)i] = fn(i);
+                if (rc[(size_t)i]) {
+                    msg[(size_t)i] = acmmp_pipeline_last_error();
+                    failed = true;
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < lanes; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto &t : pool) t.join();
+        for (int i = 0; i < num_images; ++i)
+            if (rc[(size_t)i]) {
+                pass_error = msg[(size_t)i];
+                return false;
+            }
+        return true;
+    };
     auto run_pass = [&](bool geom, bool planar, bool hier, bool multi, bool seeded = false) -> bool {
         opt.seeded = seeded;
         opt.geom_consistency = geom;
@@ -200,33 +229,13 @@ int main(int argc, char **argv) {
         // `concurrent_views` of them run at once, each with its own engine and
         // HIP stream (one view's host I/O and prior construction overlap
         // another's kernels), with the outputs of the one-at-a-time loop.
-        const int lanes = (geom && multi) ? 1 : std::max(1, std::min(concurrent_views, num_images));
-        std::vector<int> rc((size_t)num_images, 0);
-        std::vector<std::string> msg((size_t)num_images);
-        std::atomic<int> next{0};
-        std::atomic<bool> failed{false};
-        auto worker = [&] {
-            for (int i; !failed.load() && (i = next.fetch_add(1)) < num_images;) {
-                acmmp_pass_options o = opt;
-                o.seed_lo = seed + (unsigned)problems[(size_t)i].ref_image_id;
-                rc[(size_t)i] = acmmp_process_problem(dense_folder.c_str(), output_folder.c_str(), problems.data(),
-                                                      num_images, i, &o);
-                if (rc[(size_t)i]) {
-                    msg[(size_t)i] = acmmp_pipeline_last_error();
-                    failed = true;
-                }
-            }
-        };
-        std::vector<std::thread> pool;
-        for (int t = 1; t < lanes; ++t) pool.emplace_back(worker);
-        worker();
-        for (auto &t : pool) t.join();
-        for (int i = 0; i < num_images; ++i)
-            if (rc[(size_t)i]) {
-                pass_error = msg[(size_t)i];
-                return false;
-            }
-        return true;
+        const int lanes = (geom && multi) ? 1 : concurrent_views;
+        return for_views(lanes, [&](int i) {
+            acmmp_pass_options o = opt;
+            o.seed_lo = seed + (unsigned)problems[(size_t)i].ref_image_id;
+            return acmmp_process_problem(dense_folder.c_str(), output_folder.c_str(), problems.data(), num_images, i,
+                                         &o);
+        });
     };
     auto die_pass = [&](const char *what) {
         std::fprintf(stderr, "acmmp_main: %s: %s\n", what, pass_error.c_str());
@@ -271,10 +280,13 @@ int main(int argc, char **argv) {
             if (!run_pass(false, true, false, false, prior)) return die_pass("ProcessProblem");
         } else {
             if (!quiet) std::printf("Starting JBU\n");
-            for (auto &p : problems)
-                if (acmmp_joint_bilateral_upsampling(dense_folder.c_str(), output_folder.c_str(), &p,
-                                                     p.cur_image_size, device))
-                    return die("JointBilateralUpsampling");
+            // each view upsamples its own coarse map into its own folder: independent
+            if (!for_views(concurrent_views, [&](int i) {
+                    const acmmp_problem &p = problems[(size_t)i];
+                    return acmmp_joint_bilateral_upsampling(dense_folder.c_str(), output_folder.c_str(), &p,
+                                                            p.cur_image_size, device);
+                }))
+                return die_pass("JointBilateralUpsampling");
             if (!run_pass(false, true, true, false)) return die_pass("ProcessProblem");
         }
         for (int g = 0; g < geom_iterations; ++g)
