@@ -139,20 +139,24 @@ def run_sequential(dense_folder: str, output_dir: str | None = None, device: int
     os.makedirs(output_folder, exist_ok=True)
     state = {"pass": 0}
 
+    def for_views(lanes, fn):
+        """fn(0..n-1), `lanes` at a time; the first failing view in order
+        raises, as the one-at-a-time loop would."""
+        lanes = max(1, min(lanes, len(problems)))
+        if lanes == 1:
+            for i in range(len(problems)):
+                fn(i)
+            return
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(lanes) as ex:
+            for f in [ex.submit(fn, i) for i in range(len(problems))]:
+                f.result()
+
     def run_pass(geom, planar, hier, multi, seeded=False):
         opts = [pass_options(geom, planar, hier, multi, device, max_iterations, seed + p.ref_image_id,
                              state["pass"], write_triangulation, verbose, seeded) for p in problems]
-        lanes = 1 if (geom and multi) else max(1, min(concurrent_views, len(problems)))
-        if lanes == 1:
-            for i in range(len(problems)):
-                process_problem(dense_folder, output_folder, problems, i, opts[i])
-        else:
-            from concurrent.futures import ThreadPoolExecutor
-            with ThreadPoolExecutor(lanes) as ex:
-                futs = [ex.submit(process_problem, dense_folder, output_folder, problems, i, opts[i])
-                        for i in range(len(problems))]
-                for f in futs:  # the first failing view in order, as the loop reports it
-                    f.result()
+        for_views(1 if (geom and multi) else concurrent_views,
+                  lambda i: process_problem(dense_folder, output_folder, problems, i, opts[i]))
         state["pass"] += 1
 
     first = True
@@ -162,8 +166,9 @@ def run_sequential(dense_folder: str, output_dir: str | None = None, device: int
             first = False
             run_pass(False, True, False, False, prior)
         else:
-            for p in problems:
-                joint_bilateral_upsampling(dense_folder, output_folder, p, p.cur_image_size, device)
+            # each view upsamples its own coarse map into its own folder
+            for_views(concurrent_views, lambda i: joint_bilateral_upsampling(
+                dense_folder, output_folder, problems[i], problems[i].cur_image_size, device))
             run_pass(False, True, True, False)
         for g in range(geom_iterations):
             run_pass(True, False, False, g > 0)
