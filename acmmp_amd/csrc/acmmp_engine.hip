@@ -69,6 +69,70 @@ void pinned_kv_free(KViews *p) {
     (void)hipHostFree(p);
 }
 
+// An engine's stream and events, kept for the next engine on the device when
+// it is destroyed (creating and destroying them costs a few milliseconds per
+// ProcessProblem); only idle handles are kept: acmmp_destroy synchronises the
+// stream first. Off with the block cache (ACMMP_DEVICE_POOL_MB=0).
+struct HandlePool {
+    std::mutex mu;
+    std::map<int, std::vector<hipStream_t>> streams;
+    std::map<std::pair<int, bool>, std::vector<hipEvent_t>> events;  // (device, timed)
+};
+HandlePool &handles() {
+    static HandlePool *p = new HandlePool();
+    return *p;
+}
+
+hipError_t stream_take(int dev, hipStream_t *s) {
+    if (devpool().cap) {
+        std::lock_guard<std::mutex> g(handles().mu);
+        auto &v = handles().streams[dev];
+        if (!v.empty()) {
+            *s = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+void stream_give(int dev, hipStream_t s) {
+    if (devpool().cap) {
+        std::lock_guard<std::mutex> g(handles().mu);
+        auto &v = handles().streams[dev];
+        if (v.size() < 16) {
+            v.push_back(s);
+            return;
+        }
+    }
+    (void)hipStreamDestroy(s);
+}
+
+hipError_t event_take(int dev, bool timed, hipEvent_t *e) {
+    if (devpool().cap) {
+        std::lock_guard<std::mutex> g(handles().mu);
+        auto &v = handles().events[{dev, timed}];
+        if (!v.empty()) {
+            *e = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    return timed ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
+}
+
+void event_give(int dev, bool timed, hipEvent_t e) {
+    if (devpool().cap) {
+        std::lock_guard<std::mutex> g(handles().mu);
+        auto &v = handles().events[{dev, timed}];
+        if (v.size() < 256) {
+            v.push_back(e);
+            return;
+        }
+    }
+    (void)hipEventDestroy(e);
+}
+
 }  // namespace
 
 hipError_t acmmp::dev_alloc(void **p, size_t bytes) {
@@ -231,7 +295,7 @@ int kv_upload(acmmp_ctx *ctx) {
     if (!ctx->d_kv_ring[k]) {
         HIP_TRY(ctx, dalloc(ctx->d_kv_ring[k], 1));
         HIP_TRY(ctx, pinned_kv_alloc(&ctx->h_kv_ring[k]));
-        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->kv_ev[k], hipEventDisableTiming));
+        HIP_TRY(ctx, event_take(ctx->device, false, &ctx->kv_ev[k]));
     }
     if (ctx->kv_used[k]) HIP_TRY(ctx, hipEventSynchronize(ctx->kv_ev[k]));
     std::memcpy(ctx->h_kv_ring[k], &kv, sizeof(KViews));
@@ -537,7 +601,7 @@ int acmmp_create(int device, acmmp_ctx **out) {
     acmmp_ctx *ctx = new acmmp_ctx();
     ctx->device = device;
     acmmp_default_params(&ctx->prm);
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (stream_take(device, &ctx->stream) != hipSuccess) {
         delete ctx;
         return ACMMP_ERR_HIP;
     }
@@ -559,12 +623,12 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     g_frees_synced = false;
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
         if (ctx->h_kv_ring[k]) pinned_kv_free(ctx->h_kv_ring[k]);
-        if (ctx->kv_ev[k]) (void)hipEventDestroy(ctx->kv_ev[k]);
+        if (ctx->kv_ev[k]) event_give(ctx->device, false, ctx->kv_ev[k]);
     }
     if (ctx->events_made)
-        for (auto &e : ctx->ev) (void)hipEventDestroy(e);
-    if (ctx->wait_ev) (void)hipEventDestroy(ctx->wait_ev);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        for (auto &e : ctx->ev) event_give(ctx->device, true, e);
+    if (ctx->wait_ev) event_give(ctx->device, false, ctx->wait_ev);
+    if (ctx->stream) stream_give(ctx->device, ctx->stream);
     delete ctx;
 }
 
@@ -746,7 +810,7 @@ int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, co
 int acmmp_wait_stream(acmmp_ctx *ctx, void *stream) {
     if (!ctx) return ACMMP_ERR_ARG;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (!ctx->wait_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->wait_ev, hipEventDisableTiming));
+    if (!ctx->wait_ev) HIP_TRY(ctx, event_take(ctx->device, false, &ctx->wait_ev));
     // hipStreamWaitEvent captures the event's state at this call, so the one
     // event is safely re-recorded by the next call
     HIP_TRY(ctx, hipEventRecord(ctx->wait_ev, (hipStream_t)stream));
@@ -878,7 +942,7 @@ int prepare_run(acmmp_ctx *ctx) {
     if (p.texture_filter8 && (ctx->pad_texel == kTexelH16 || ctx->h_kv.wide))
         return set_err(ctx, ACMMP_ERR_UNSUPPORTED, "texture_filter8 is built for the u8 / fp32 texel forms below 2^24 records");
     if (ctx->timing && !ctx->events_made) {
-        for (auto &e : ctx->ev) HIP_TRY(ctx, hipEventCreate(&e));
+        for (auto &e : ctx->ev) HIP_TRY(ctx, event_take(ctx->device, true, &e));
         ctx->events_made = true;
     }
     return ACMMP_OK;

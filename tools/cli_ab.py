@@ -2,7 +2,8 @@
 (tools/pipeline_times.write_cfg4_dense): each round runs every binary once,
 in order, into its own output folder.
 
-usage: python tools/cli_ab.py <rounds> <binary> [<binary> ...] > gpurun_out/cli_ab.jsonl
+usage: python tools/cli_ab.py <rounds> <side> [<side> ...] > gpurun_out/cli_ab.jsonl
+  side: <binary> or VAR=value@<binary> (one environment variable for that side)
 """
 import json
 import os
@@ -21,12 +22,16 @@ def main():
     rounds, bins = int(sys.argv[1]), sys.argv[2:]
     tmp, dense = write_cfg4_dense(49, 1600, 1200, 20)
     for r in range(rounds):
-        for k, b in enumerate(bins):
+        for k, side in enumerate(bins):
+            env = dict(os.environ)
+            b = side
+            if "@" in side:
+                var, b = side.split("@", 1)
+                env[var.split("=", 1)[0]] = var.split("=", 1)[1]
             out = "/ACMMP_ab%d" % k
             t0 = time.perf_counter()
-            subprocess.run([b, dense, "--output_dir", out, "--no_fusion", "--quiet"], check=True)
-            print(json.dumps({"round": r, "binary": os.path.basename(b), "s": round(time.perf_counter() - t0, 2)}),
-                  flush=True)
+            subprocess.run([b, dense, "--output_dir", out, "--no_fusion", "--quiet"], check=True, env=env)
+            print(json.dumps({"round": r, "side": side, "s": round(time.perf_counter() - t0, 2)}), flush=True)
             shutil.rmtree(dense + out, ignore_errors=True)
     shutil.rmtree(tmp, ignore_errors=True)
 
