@@ -1179,20 +1179,29 @@ int acmmp_joint_bilateral_upsample(int device, const float *image, int width, in
     if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
     const size_t P = (size_t)width * height, S = (size_t)depth_width * depth_height;
     float *d_img = nullptr, *d_dep = nullptr, *d_out = nullptr;
+    // the stream and blocks come from the engines' caches and return there
+    // once the stream is synchronised (hipFree would synchronise the device)
     hipStream_t s = nullptr;
-    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc((void **)&d_img, P * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc((void **)&d_dep, S * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc((void **)&d_out, P * sizeof(float));
+    hipError_t e = stream_take(device, &s);
+    if (e == hipSuccess) e = dalloc(d_img, P);
+    if (e == hipSuccess) e = dalloc(d_dep, S);
+    if (e == hipSuccess) e = dalloc(d_out, P);
     if (e == hipSuccess) e = hipMemcpyAsync(d_img, image, P * sizeof(float), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_dep, depth, S * sizeof(float), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = launch_jbu(d_img, width, height, d_dep, depth_width, depth_height, isc, d_out, s);
     if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, P * sizeof(float), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (d_img) (void)hipFree(d_img);
-    if (d_dep) (void)hipFree(d_dep);
-    if (d_out) (void)hipFree(d_out);
-    if (s) (void)hipStreamDestroy(s);
+    if (e == hipSuccess) {
+        dfree_synced(d_img);
+        dfree_synced(d_dep);
+        dfree_synced(d_out);
+        stream_give(device, s);
+    } else {  // a failed stream may still hold work: the plain frees
+        dfree(d_img);
+        dfree(d_dep);
+        dfree(d_out);
+        if (s) (void)hipStreamDestroy(s);
+    }
     return e == hipSuccess ? ACMMP_OK : ACMMP_ERR_HIP;
 }
 
