@@ -162,6 +162,8 @@ SIGNATURES = {
     "acmmp_default_params": (None, [C.POINTER(Params)]),
     "acmmp_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "acmmp_destroy": (None, [_CTX]),
+    "acmmp_release_device_cache": (C.c_int, [C.c_int]),
+    "acmmp_device_cache_bytes": (C.c_int64, [C.c_int]),
     "acmmp_last_error": (C.c_char_p, [_CTX]),
     "acmmp_set_params": (C.c_int, [_CTX, C.POINTER(Params)]),
     "acmmp_get_params": (C.c_int, [_CTX, C.POINTER(Params)]),

@@ -33,7 +33,32 @@ struct DevPool {
     size_t cached = 0, cap = 0;
     DevPool() {
         const char *e = std::getenv("ACMMP_DEVICE_POOL_MB");
-        cap = (size_t)(e ? std::atoll(e) : 8192) << 20;
+        const long long mb = e ? std::atoll(e) : 8192;
+        cap = (size_t)std::max(0LL, mb) << 20;  // a negative setting means off, not a huge cap
+    }
+    // hipFree of every cached block of device dev (all devices: dev < 0);
+    // caller holds mu. Returns the bytes given back.
+    size_t release(int dev) {
+        size_t n = 0;
+        for (auto it = free_.begin(); it != free_.end();) {
+            if (dev >= 0 && it->first.first != dev) {
+                ++it;
+                continue;
+            }
+            for (void *p : it->second) {
+                (void)hipFree(p);
+                n += it->first.second;
+            }
+            it = free_.erase(it);
+        }
+        cached -= n;
+        return n;
+    }
+    size_t bytes(int dev) const {
+        size_t n = 0;
+        for (const auto &kv : free_)
+            if (dev < 0 || kv.first.first == dev) n += kv.first.second * kv.second.size();
+        return n;
     }
 };
 DevPool &devpool() {
@@ -150,7 +175,21 @@ hipError_t acmmp::dev_alloc(void **p, size_t bytes) {
             return hipSuccess;
         }
     }
-    const hipError_t e = hipMalloc(p, bytes);
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) {
+        // the cache may hold what the device lacks: give this device's
+        // cached blocks back and try once more
+        (void)hipGetLastError();
+        size_t freed = 0;
+        {
+            std::lock_guard<std::mutex> g(pool.mu);
+            freed = pool.release(dev);
+        }
+        if (freed) {
+            e = hipMalloc(p, bytes);
+            if (e != hipSuccess) (void)hipGetLastError();
+        }
+    }
     if (e == hipSuccess) {
         std::lock_guard<std::mutex> g(pool.mu);
         pool.size_of[*p] = bytes;
@@ -612,9 +651,15 @@ int acmmp_create(int device, acmmp_ctx **out) {
 void acmmp_destroy(acmmp_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    // nothing queued can touch the engine's blocks now: they go to the cache
-    g_frees_synced = true;
+    // Only a stream that drained cleanly hands its blocks, staging and
+    // handles on to the next engine: after a failed sync (an asynchronous
+    // error, a stream that did not drain) queued work may still touch them,
+    // so they are released with hipFree / hipStreamDestroy (which wait for the
+    // device) instead. Work the CALLER queued on other streams that reads
+    // this engine's buffers must be finished before this call (include/acmmp.h).
+    const bool clean = !ctx->stream || hipStreamSynchronize(ctx->stream) == hipSuccess;
+    if (!clean) (void)hipGetLastError();
+    g_frees_synced = clean;  // nothing queued can touch the engine's blocks now: they go to the cache
     free_images(ctx);
     free_state(ctx);
     for (auto &p : ctx->pad) dfree(p);
@@ -622,14 +667,70 @@ void acmmp_destroy(acmmp_ctx *ctx) {
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) dfree(ctx->d_kv_ring[k]);
     g_frees_synced = false;
     for (int k = 0; k < acmmp_ctx::kSlots; ++k) {
-        if (ctx->h_kv_ring[k]) pinned_kv_free(ctx->h_kv_ring[k]);
-        if (ctx->kv_ev[k]) event_give(ctx->device, false, ctx->kv_ev[k]);
+        if (ctx->h_kv_ring[k]) {
+            if (clean) pinned_kv_free(ctx->h_kv_ring[k]);
+            else (void)hipHostFree(ctx->h_kv_ring[k]);
+        }
+        if (ctx->kv_ev[k]) {
+            if (clean) event_give(ctx->device, false, ctx->kv_ev[k]);
+            else (void)hipEventDestroy(ctx->kv_ev[k]);
+        }
     }
     if (ctx->events_made)
-        for (auto &e : ctx->ev) event_give(ctx->device, true, e);
-    if (ctx->wait_ev) event_give(ctx->device, false, ctx->wait_ev);
-    if (ctx->stream) stream_give(ctx->device, ctx->stream);
+        for (auto &e : ctx->ev) {
+            if (clean) event_give(ctx->device, true, e);
+            else (void)hipEventDestroy(e);
+        }
+    if (ctx->wait_ev) {
+        if (clean) event_give(ctx->device, false, ctx->wait_ev);
+        else (void)hipEventDestroy(ctx->wait_ev);
+    }
+    if (ctx->stream) {
+        if (clean) stream_give(ctx->device, ctx->stream);
+        else (void)hipStreamDestroy(ctx->stream);
+    }
     delete ctx;
+}
+
+int acmmp_release_device_cache(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ACMMP_ERR_HIP;
+    if (device >= ndev || device < -1) return ACMMP_ERR_ARG;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    {
+        DevPool &pool = devpool();
+        std::lock_guard<std::mutex> g(pool.mu);
+        pool.release(device);
+    }
+    {
+        std::lock_guard<std::mutex> g(handles().mu);
+        for (auto it = handles().streams.begin(); it != handles().streams.end(); ++it) {
+            if (device >= 0 && it->first != device) continue;
+            (void)hipSetDevice(it->first);
+            for (hipStream_t s : it->second) (void)hipStreamDestroy(s);
+            it->second.clear();
+        }
+        for (auto it = handles().events.begin(); it != handles().events.end(); ++it) {
+            if (device >= 0 && it->first.first != device) continue;
+            (void)hipSetDevice(it->first.first);
+            for (hipEvent_t e : it->second) (void)hipEventDestroy(e);
+            it->second.clear();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(g_pinned_mu);  // host staging is not per device: released with any call
+        for (KViews *p : g_pinned_kv) (void)hipHostFree(p);
+        g_pinned_kv.clear();
+    }
+    (void)hipSetDevice(cur);
+    return ACMMP_OK;
+}
+
+int64_t acmmp_device_cache_bytes(int device) {
+    DevPool &pool = devpool();
+    std::lock_guard<std::mutex> g(pool.mu);
+    return (int64_t)pool.bytes(device);
 }
 
 const char *acmmp_last_error(const acmmp_ctx *ctx) {

@@ -103,6 +103,41 @@ float get_angle(const float *a, const float *b) {  // GetAngle
     return angle;
 }
 
+// RunFusion phase 1's two arithmetic stages (see phase1 below): branch-free
+// loops the vectoriser turns into AVX2 where the host has it. Each is built
+// twice (target_clones: an AVX2 clone and a baseline x86-64 clone, picked by
+// the loader from the running CPU), so the library never executes an AVX2
+// instruction on a host without it. AVX2 without FMA, and this file builds
+// with -ffp-contract=off: both clones perform the same IEEE operations, so
+// the PLY does not depend on the host.
+__attribute__((target_clones("avx2", "default")))
+void stage_project(const F3 *X, size_t nl, const acmmp_camera &cs, int *scp, int *srp) {
+    for (size_t k = 0; k < nl; ++k) {
+        float ptx, pty, proj_depth;
+        project(X[k], cs, ptx, pty, proj_depth);
+        srp[k] = int(pty + 0.5f);
+        scp[k] = int(ptx + 0.5f);
+    }
+}
+
+// reprojection of candidate q's source pixel into view i (row r): error and
+// relative depth difference
+__attribute__((target_clones("avx2", "default")))
+void stage_reproject(size_t nc, int r, const int *__restrict__ col, const int *__restrict__ scp,
+                     const int *__restrict__ srp, const float *__restrict__ cd, const float *__restrict__ cr,
+                     float *__restrict__ re, float *__restrict__ rd, const acmmp_camera cs, const acmmp_camera ci) {
+    for (size_t q = 0; q < nc; ++q) {
+        const float ref_depth = cr[q];
+        float tx, ty, proj_depth;
+        const F3 tmp_X = world_point(scp[q], srp[q], cd[q], cs);
+        project(tmp_X, ci, tx, ty, proj_depth);
+        // std::pow(v, 2) of a float v is exact in double: v * v
+        const double dx = (double)(col[q] - tx), dy = (double)(r - ty);
+        re[q] = (float)std::sqrt(dx * dx + dy * dy);
+        rd[q] = std::fabs(proj_depth - ref_depth) / ref_depth;
+    }
+}
+
 // RunFusion's threads kept on ONE last-level-cache domain (on a many-CCD
 // host a view's candidate lists, written by the pool, and the masks, written
 // by the walk, otherwise cross between L3s on every access; the walk, which
@@ -704,17 +739,7 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             // the two arithmetic stages are branch-free loops the compiler
             // vectorises; the gathers and the mask reads stay scalar).
             // (1) the projection into the source
-            {
-                const F3 *X = rs.X.data();
-                int *scp = rs.src_c.data(), *srp = rs.src_r.data();
-                const acmmp_camera &cs = cameras[s];
-                for (size_t k = 0; k < nl; ++k) {
-                    float ptx, pty, proj_depth;
-                    project(X[k], cs, ptx, pty, proj_depth);
-                    srp[k] = int(pty + 0.5f);
-                    scp[k] = int(ptx + 0.5f);
-                }
-            }
+            stage_project(rs.X.data(), nl, cameras[s], rs.src_c.data(), rs.src_r.data());
             // (2) in bounds, unmasked, positive source depth: the candidates,
             // with what stage 3 reads, in contiguous arrays
             rs.cand.resize(nl);
@@ -743,23 +768,8 @@ int acmmp_run_fusion(const char *dense_folder, const char *output_folder, const 
             // (3) the reprojection into view i: error and relative depth difference
             rs.rerr.resize(nc);
             rs.rdiff.resize(nc);
-            {
-                const int *__restrict__ col = rs.ccol.data(), *__restrict__ scp = rs.csc.data();
-                const int *__restrict__ srp = rs.csr.data();
-                const float *__restrict__ cd = rs.cdepth.data(), *__restrict__ cr = rs.cref.data();
-                float *__restrict__ re = rs.rerr.data(), *__restrict__ rd = rs.rdiff.data();
-                const acmmp_camera cs = cameras[s], ci = cameras[i];
-                for (size_t q = 0; q < nc; ++q) {
-                    const float ref_depth = cr[q];
-                    float tx, ty, proj_depth;
-                    const F3 tmp_X = world_point(scp[q], srp[q], cd[q], cs);
-                    project(tmp_X, ci, tx, ty, proj_depth);
-                    // std::pow(v, 2) of a float v is exact in double: v * v
-                    const double dx = (double)(col[q] - tx), dy = (double)(r - ty);
-                    re[q] = (float)std::sqrt(dx * dx + dy * dy);
-                    rd[q] = std::fabs(proj_depth - ref_depth) / ref_depth;
-                }
-            }
+            stage_reproject(nc, r, rs.ccol.data(), rs.csc.data(), rs.csr.data(), rs.cdepth.data(), rs.cref.data(),
+                            rs.rerr.data(), rs.rdiff.data(), cameras[s], cameras[i]);
             // (4) the reference evaluates all three before the test; acos is
             // pure, so the angle is only formed where the first two pass
             for (size_t q = 0; q < nc; ++q) {

@@ -49,6 +49,28 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
+// Timing-only upper bounds (A/B builds only, wrong results): the current
+// plane's NCC calls skipped (its stored cost stands in), or the refinement's.
+#ifndef ACMMP_UB_SKIP_NOW
+#define ACMMP_UB_SKIP_NOW 0
+#endif
+#ifndef ACMMP_UB_SKIP_REFINE
+#define ACMMP_UB_SKIP_REFINE 0
+#endif
+// (bounds on the refinement's packing, all with its results discarded so no
+// refinement plane is ever accepted and the downstream work is the same:
+// DISCARD alone = the product's evaluation; ALWAYS_FAST = every NCC takes the
+// Newton-reciprocal path; XVIEW_PACK = the items of all views packed into
+// full-wave passes as if they were one view's, i.e. ideal cross-view packing)
+#ifndef ACMMP_UB_REFINE_DISCARD
+#define ACMMP_UB_REFINE_DISCARD 0
+#endif
+#ifndef ACMMP_UB_ALWAYS_FAST
+#define ACMMP_UB_ALWAYS_FAST 0
+#endif
+#ifndef ACMMP_UB_XVIEW_PACK
+#define ACMMP_UB_XVIEW_PACK 0
+#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -694,7 +716,8 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     const float z11 = dm_fma(H[7], yb, dm_fma(H[6], xr, H[8]));
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
-    const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
+    const bool fast = ACMMP_UB_ALWAYS_FAST ||
+                      (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
     if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     sum_src *= pp.inv_wsum;
@@ -1112,7 +1135,35 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
     const int nact = __popcll(act), arank = __popcll(act & lt);
     float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     wave_sync();
-    for (int j = 0; j < nsrc; ++j) {
+    if (ACMMP_UB_XVIEW_PACK) {
+        int total = 0;
+        for (int j = 0; j < nsrc; ++j) total += __popcll(__ballot(vw.get(j) > 0));
+        cmp_list(lds, wbase + arank) = lane;
+        wave_sync();
+        const int n = 5 * total;
+        for (int base = 0; base < n; base += nact) {
+            const int k = base + arank;
+            if (k < n) {
+                const int t = k % 5;
+                const int otid = wbase + cmp_list(lds, wbase + (k / 5) % nact);
+                const LaneGeom og = lane_geom_of(colour, blk, otid);
+                PixPatch op;
+                op.wo = otid;
+                op.w = wlds + otid;
+                op.rt = tile + og.tb;
+                op.mean = cmp_pd(lds, 1, otid);
+                op.var = cmp_pd(lds, 2, otid);
+                op.inv_wsum = cmp_pd(lds, 3, otid);
+                const float4 h = lds[t * kThreads + otid];
+                GeomFetch gf = {};
+                if (kv.prm.geom_consistency) gf = geom_fetch(kv, 1, geom_ref(kv, h, og.px, og.py));
+                const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, 1, og.px, og.py, h);
+                cmp_res(lds, t, otid) = kv.prm.geom_consistency ? cc + 0.2f * geom_finish(kv, 1, gf, og.px, og.py) : cc;
+            }
+        }
+        wave_sync();
+    }
+    for (int j = 0; j < nsrc && !ACMMP_UB_XVIEW_PACK; ++j) {
         const float wj = (float)vw.get(j);
         const uint64_t m = __ballot(wj > 0);
         if (m == 0) continue;
@@ -1122,7 +1173,7 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
         const int n = 5 * c;
         for (int base = 0; base < n; base += nact) {
             const int k = base + arank;
-            if (k < n) {
+            if (k < n && !ACMMP_UB_SKIP_REFINE) {
                 const int t = k / c;
                 const int otid = wbase + cmp_list(lds, wbase + (k - t * c));
                 const LaneGeom og = lane_geom_of(colour, blk, otid);
@@ -1151,9 +1202,16 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
         wave_sync();
         if (wj > 0) {
 #pragma unroll
-            for (int t = 0; t < 5; ++t) acc[t] += wj * cmp_res(lds, t, tid);
+            for (int t = 0; t < 5; ++t)
+                acc[t] += wj * ((ACMMP_UB_SKIP_REFINE || ACMMP_UB_REFINE_DISCARD) ? 2.0f : cmp_res(lds, t, tid));
         }
         wave_sync();
+    }
+    if (ACMMP_UB_XVIEW_PACK) {
+        float wn = 0.0f;
+        for (int j = 0; j < nsrc; ++j) wn += (float)vw.get(j);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t] = 2.0f * wn;
     }
 #pragma unroll
     for (int t = 0; t < 5; ++t) cmp_res(lds, t, tid) = acc[t];
@@ -1520,6 +1578,8 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         float tc = 0.0f;
         if (t >= 1) {
             tc = cmp_res(cand_lds, t - 1, pp.wo);
+        } else if (ACMMP_UB_SKIP_NOW) {
+            tc = my_cost * weight_norm;  // timing-only bound: the stored cost stands in (wrong results)
         } else {
         GeomRef gnow = {};
         if (prm.geom_consistency) gnow = geom_ref(kv, h, px, py);  // once for the current plane

@@ -137,6 +137,20 @@ def device_count() -> int:
     return int(_abi.load_library().acmmp_device_count())
 
 
+def release_device_cache(device: int = -1) -> None:
+    """Gives the library's cached device blocks (and idle streams/events) of
+    `device` (-1: every device) back to the HIP runtime
+    (acmmp_release_device_cache)."""
+    rc = _abi.load_library().acmmp_release_device_cache(int(device))
+    if rc != _abi.OK:
+        raise AcmmpError(f"acmmp_release_device_cache({device}) failed with status {rc}")
+
+
+def device_cache_bytes(device: int = -1) -> int:
+    """Bytes of device blocks the library's cache holds (acmmp_device_cache_bytes)."""
+    return int(_abi.load_library().acmmp_device_cache_bytes(int(device)))
+
+
 class ACMMP:
     """One PatchMatch engine bound to one GPU (`ACMMP acmmp;` +
     `cudaSetDevice`, src/acmmp_definitions.cpp:253-260)."""

@@ -159,15 +159,26 @@ class ResidentViews:
     the cfg2 parity test's (tests/test_gpu_headline.py)."""
 
     def __init__(self, pool: EnginePool, cams: dict, images: dict, sources: dict, mine: Sequence[int],
-                 height: int, width: int, total_views: Optional[int] = None, base_id: int = 0):
+                 height: int, width: int, total_views: Optional[int] = None, base_id: int = 0,
+                 view_seed: Optional[int] = None):
         import torch
         from .engine import Texture
         self.pool = pool
         self.cams, self.images, self.sources = cams, images, sources
-        # one texture per image, shared by every view, engine and pass
-        self.textures = {i: Texture.of(im, pool.device) for i, im in images.items()}
+        # one texture per image tensor, shared by every view id that maps to
+        # it (bench.py's rank copies of one scene), engine and pass
+        by_tensor = {}
+        self.textures = {}
+        for i, im in images.items():
+            key = (im.data_ptr(), tuple(im.shape))
+            if key not in by_tensor:
+                by_tensor[key] = Texture.of(im, pool.device)
+            self.textures[i] = by_tensor[key]
         self.mine = list(mine)
         self.base_id = base_id
+        # view_seed: every view's Philox key is view_seed + its global id (as
+        # the pass drivers key seed + ref_image_id), else the params' own key
+        self.view_seed = view_seed
         dev = next(iter(images.values())).device
         n = len(self.mine)
         self.planes = torch.empty((n, height, width, 4), dtype=torch.float32, device=dev)
@@ -184,12 +195,20 @@ class ResidentViews:
     def _depth_index(self, i):
         return i if self.all_depth is not self.my_depth else self.mine.index(i)
 
+    def _params_of(self, params: _abi.Params, v: int) -> _abi.Params:
+        if self.view_seed is None:
+            return params
+        p = type(params).from_buffer_copy(params)
+        p.seed_lo = (self.view_seed + v) & 0xFFFFFFFF
+        return p
+
     def photometric_pass(self, params: _abi.Params):
         def one(eng, kv):
             k, v = kv
             ids = self._ids(v)
             self.used_params[("photo", v)] = photometric_view(
-                self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
+                self.pool, eng, self._params_of(params, v), [self.cams[i] for i in ids],
+                [self.images[i].data_ptr() for i in ids],
                 self.planes[k].data_ptr(), self.costs[k].data_ptr(), self.my_depth[k].data_ptr(),
                 textures=[self.textures[i] for i in ids])
         self.pool.map(one, list(enumerate(self.mine)))
@@ -202,7 +221,8 @@ class ResidentViews:
             k, v = kv
             ids = self._ids(v)
             self.used_params[("geom", v)] = geometric_view(
-                self.pool, eng, params, [self.cams[i] for i in ids], [self.images[i].data_ptr() for i in ids],
+                self.pool, eng, self._params_of(params, v), [self.cams[i] for i in ids],
+                [self.images[i].data_ptr() for i in ids],
                 [self.all_depth[self._depth_index(i)].data_ptr() for i in ids],
                 self.planes[k].data_ptr(), self.costs[k].data_ptr(), textures=[self.textures[i] for i in ids])
         self.pool.map(one, list(enumerate(self.mine)))

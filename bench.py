@@ -11,8 +11,14 @@ One "step" = photometric pass + all-gather + geometric pass, run by
 `acmmp_amd.resident` (the same code the parity test
 tests/test_gpu_headline.py drives): images, plane/cost state and depth maps
 stay in HBM, every RunPatchMatch's results are exported device-to-device.
-Weak scaling: every rank owns one copy of the 10-view cfg2 problem (global
-view ids rank*10 + k), so per-GPU work is identical for every N.
+Weak scaling: every rank owns one copy of the 10-view cfg2 scene (global
+view ids rank*10 + k), so per-GPU work is identical for every N. Sources span
+ranks as the reference's pair lists span views (src/ACMMP.cpp:619-634): source
+j of view (r, k) is scene view pairs[k][j] as held by rank (r + 1 + j) mod N,
+and every view has its own Philox key (1234 + global id, as the pass drivers
+key seed + ref_image_id), so the copies' depth maps differ and each geometric
+pass reads other ranks' gathered maps (at N = 1 every source is the rank's
+own view, as before).
 
 value = RunPatchMatch pixels processed by all ranks (2 passes x views x W x H)
 / max-over-ranks wall time of the K timed steps, in Mpix/s (per pass; a
@@ -69,7 +75,24 @@ def parse(argv=None):
     ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
                     help="in-run rocprofv3 counter passes for the roofline (rank 0, N=1)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    # tests only (tests/test_gpu_bench_exchange.py): one process holding the
+    # views of every rank of a world of this size, no collective; and the
+    # final state of every owned view saved as .npy files
+    ap.add_argument("--emulate-ranks", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--dump", default="", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+VIEW_SEED = 1234  # Philox key of global view g: VIEW_SEED + g (acmmp_params.seed_lo)
+
+
+def view_sources(k: int, rank: int, world: int, views: int, pairs, nsrc: int) -> list:
+    """Global source ids of reference view k of `rank`: source j is scene
+    view pairs[k][j] as held by rank (rank + 1 + j) mod world, so a rank's
+    geometric pass reads the gathered depth maps of the other ranks (the
+    reference's source lists span views, src/ACMMP.cpp:619-634; at world 1
+    every source is the rank's own copy)."""
+    return [((rank + 1 + j) % world) * views + pairs[k][j] for j in range(nsrc)]
 
 
 def host_cpu():
@@ -128,19 +151,27 @@ def main():
     if args.views < args.nsrc + 1:
         raise SystemExit(f"--views {args.views} cannot supply {args.nsrc} source views per problem")
     streams = 1 if args.pmc_child else args.streams
-    V = args.views * world
+    emulate = args.emulate_ranks if (args.emulate_ranks > 1 and not distributed) else 0
+    views_world = emulate or world  # ranks whose views the global view set holds
+    V = args.views * views_world
     W, H = args.width, args.height
     setup = scene.scene_setup(num_views=args.views, width=W, height=H)
-    base_id = rank * args.views
-    mine = list(range(base_id, base_id + args.views))
-    srcs = {base_id + k: [base_id + j for j in setup.pairs[k][:args.nsrc]] for k in range(args.views)}
-    images = {base_id + k: scene.render_torch(setup, k, device) for k in range(args.views)}
-    cams = {base_id + k: setup.camera(k) for k in range(args.views)}
+    here = range(emulate) if emulate else [rank]  # the ranks whose views this process owns
+    mine = [r * args.views + k for r in here for k in range(args.views)]
+    srcs = {r * args.views + k: view_sources(k, r, views_world, args.views, setup.pairs, args.nsrc)
+            for r in here for k in range(args.views)}
+    # a rank's copy of scene view m and every other rank's copy are the same
+    # image and camera (one rendered tensor per scene view, shared by ids)
+    rendered = {k: scene.render_torch(setup, k, device) for k in range(args.views)}
+    needed = sorted(set(mine) | {i for v in mine for i in srcs[v]})
+    images = {g: rendered[g % args.views] for g in needed}
+    cams = {g: setup.camera(g % args.views) for g in needed}
     torch.cuda.synchronize()
 
     n_img = 1 + args.nsrc
     pool = EnginePool(dev_index, streams, timing=True)
-    rv = ResidentViews(pool, cams, images, srcs, mine, H, W, total_views=V if distributed else None)
+    rv = ResidentViews(pool, cams, images, srcs, mine, H, W, total_views=V if distributed else None,
+                       view_seed=VIEW_SEED)
     all_depth = rv.all_depth
     photo_params = default_params()
     photo_params.max_iterations = args.iters
@@ -199,7 +230,15 @@ def main():
         rows = [[float(x) for x in g.cpu().tolist()] for g in gathered]
         elapsed = max(r[0] for r in rows)
     timed_ms, timed_launches = pool.sweep_ms, pool.sweep_launches
-    if args.pmc_child:
+    if args.dump:
+        # final state of every owned view: the geometric pass's planes and
+        # costs, and the photometric depth maps the exchange carried
+        os.makedirs(args.dump, exist_ok=True)
+        for k, v in enumerate(mine):
+            np.save(os.path.join(args.dump, f"geom_planes_{v:03d}.npy"), rv.planes[k].cpu().numpy())
+            np.save(os.path.join(args.dump, f"geom_costs_{v:03d}.npy"), rv.costs[k].cpu().numpy())
+            np.save(os.path.join(args.dump, f"photo_depth_{v:03d}.npy"), rv.my_depth[k].cpu().numpy())
+    if args.pmc_child or emulate:
         pool.close()
         return
 
@@ -242,6 +281,8 @@ def main():
             "geom_iters_note": f"the geometric pass runs {args.iters} iterations as BASELINE cfg2 states; the "
                                "reference's SetGeomConsistencyParams forces 2 (src/ACMMP.cpp:447-454)",
             "views_per_gpu": args.views,
+            "sources": "source j of view (rank r, k) = scene view pairs[k][j] held by rank (r + 1 + j) mod N "
+                       "(cross-rank reads in every geometric pass at N > 1); Philox key 1234 + global view id",
             "width": W,
             "height": H,
             "num_images": n_img,
@@ -257,7 +298,8 @@ def main():
             "ranks": rank_fields(rows, args.steps,
                                  ("RCCL" if backend == "nccl" else "gloo") if distributed else None),
         },
-        "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, streams),
+        "roofline": roofline(pmc, iso_ms, logical, timed_ms, timed_launches, streams, num_images=n_img,
+                             pixels_per_launch=P / 2),
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -292,7 +334,14 @@ def rank_fields(rows, steps, exchange):
     }
 
 
-def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
+def performed_bytes_per_pixel_iter(ncc_calls: float, geom: bool) -> float:
+    """The §8d byte model with the NCC calls the kernel actually performs per
+    pixel-iteration in place of the model's 14 (N-1)."""
+    return ncc_calls * (724 + (4 if geom else 0)) + 572
+
+
+def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams, num_images=10,
+             pixels_per_launch=800 * 1200):
     """The dominant kernel's roofline (k_sweep, >90 % of the step's GPU time),
     in the contract's form: bound "hbm", achieved = ALGORITHMIC bytes per
     launch (SURVEY §8d's gather-byte model: every NCC sample's texels counted
@@ -368,6 +417,32 @@ def roofline(pmc, iso_ms, logical_bytes, timed_ms, timed_launches, streams):
         },
         "pmc": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()},
     })
+    # The model counts 14 (N-1) NCC calls per pixel-iteration, as the
+    # reference computes them; the product skips the calls of views with a
+    # zero sampled weight (the reference multiplies their cost by 0 and adds
+    # it, src/ACMMP.cu:747-751, :1083-1089), so it performs fewer: measured as
+    # gather wave-instructions / waves / 36 samples (wave-level calls: a call
+    # with some lanes masked counts once, so this is an upper bound on the
+    # per-pixel calls performed).
+    waves = pmc.get("waves") or 0
+    if waves > 0 and insts > 0:
+        calls = insts / waves / 36
+        model_calls = 14 * (num_images - 1)
+        perf_bytes = pixels_per_launch * (performed_bytes_per_pixel_iter(calls, False) +
+                                          performed_bytes_per_pixel_iter(calls, True)) / 2
+        perf_gbs = perf_bytes / (iso_ms / 1e3) / 1e9
+        out.update({
+            "ncc_calls_per_pixel_iter": round(calls, 2),
+            "ncc_calls_per_pixel_iter_model": model_calls,
+            "performed_bytes_per_launch": round(perf_bytes),
+            "achieved_performed": round(perf_gbs, 1),
+            "frac_performed": round(perf_gbs / HBM_PEAK_GBS, 4),
+            "performed_note": "ncc_calls_per_pixel_iter = TA_BUFFER_READ_WAVEFRONTS_sum / SQ_WAVES / 36 (wave-level "
+                              "NCC calls the kernel issues); the model's 14 (N-1) includes the zero-weight calls "
+                              "the reference computes and discards (src/ACMMP.cu:747-751), which the product skips "
+                              "bit-exactly; frac_performed = the §8d bytes with the performed calls / launch_ms "
+                              "/ 8 TB/s",
+        })
     if "l2_hit_rate" in pmc:
         out["l2"] = {
             "hit_rate": round(pmc["l2_hit_rate"], 4),

@@ -132,8 +132,24 @@ void acmmp_default_params(acmmp_params *p);
 /* ~ `ACMMP acmmp;` (src/acmmp_definitions.cpp:260) + cudaSetDevice(0) (:253):
  * create an engine bound to HIP device `device` with its own stream. */
 int acmmp_create(int device, acmmp_ctx **out);
-/* ~ ACMMP::~ACMMP (src/ACMMP.cpp:109-152). NULL is a no-op. */
+/* ~ ACMMP::~ACMMP (src/ACMMP.cpp:109-152). NULL is a no-op. Synchronises the
+ * engine's own stream only (not the device, as the reference's cudaFree calls
+ * do): work the caller queued on OTHER streams that still reads this engine's
+ * buffers (acmmp_get_device_results pointers, band halo buffers) must be
+ * finished before this call. After a clean sync the engine's device blocks,
+ * stream and events go to a per-process cache for the next engine on the
+ * device (at most ACMMP_DEVICE_POOL_MB MiB of blocks, default 8192; 0 or a
+ * negative value turns the cache off); after a failed sync they are freed. */
 void acmmp_destroy(acmmp_ctx *ctx);
+/* Gives the device-block cache of `device` (every device: -1) back to the
+ * HIP runtime with hipFree, plus the cached streams, events and host staging
+ * blocks (the reference frees everything in its destructor; this returns the
+ * memory the cache kept beside, e.g., torch's caching allocator). Blocks of
+ * live engines are not touched. A hipMalloc that fails for lack of memory
+ * releases the device's cache and retries once by itself. */
+int acmmp_release_device_cache(int device);
+/* Bytes of device blocks the cache currently holds for `device` (-1: all). */
+int64_t acmmp_device_cache_bytes(int device);
 /* Last error message on this context ("" when none). Never NULL. */
 const char *acmmp_last_error(const acmmp_ctx *ctx);
 

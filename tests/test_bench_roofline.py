@@ -61,6 +61,39 @@ def test_bench_roofline_block():
     assert r["l2"]["hit_rate"] == 0.75 and r["l2"]["l1_to_l2_reqs_per_gather"] == 3.5
 
 
+def test_bench_roofline_performed_calls():
+    """the NCC calls the kernel performs (gather
+    wave-instructions / waves / 36) beside the model's 14 (N-1), and the
+    roofline fraction on the performed calls."""
+    import bench
+    s = bench_pmc.summarize(_passes())
+    r = bench.roofline(s, 4.0, 1.0e10, 8.0, 2, 2, num_images=10, pixels_per_launch=960000)
+    calls = 5.0e7 / 1.5e4 / 36
+    assert r["ncc_calls_per_pixel_iter"] == round(calls, 2)
+    assert r["ncc_calls_per_pixel_iter_model"] == 126
+    perf = 960000 * ((calls * 724 + 572) + (calls * 728 + 572)) / 2
+    assert r["performed_bytes_per_launch"] == round(perf)
+    assert abs(r["frac_performed"] - perf / 4.0e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-4
+    # fewer calls performed than modelled: the performed fraction is the smaller
+    assert r["frac_performed"] < bench.roofline(s, 4.0, 960000 * (126 * 726 + 572), 8.0, 2, 2)["frac"]
+
+
+def test_view_sources_span_ranks():
+    """at N > 1 every view reads sources held by other ranks;
+    at N = 1 all sources are the rank's own copies (the r05 lists)."""
+    import bench
+    pairs = {k: [(k + d) % 10 for d in range(1, 10)] for k in range(10)}
+    assert bench.view_sources(3, 0, 1, 10, pairs, 9) == pairs[3]
+    for world in (2, 4, 8):
+        for r in range(world):
+            for k in range(10):
+                src = bench.view_sources(k, r, world, 10, pairs, 9)
+                assert [g % 10 for g in src] == pairs[k]
+                owners = [g // 10 for g in src]
+                assert owners[0] == (r + 1) % world  # the nearest source always comes from the next rank
+                assert set(owners) == set(range(world))  # nine sources cover every rank of N <= 9
+
+
 def test_rank_fields():
     """The N>1 attribution block: per-rank pass times, the
     depth all-gather's ms per step and the view counts, from each rank's

@@ -5,7 +5,8 @@ streams fed from a shared queue, images borrowed from HBM
 (export_results) and fed back through set_depth_maps_device /
 set_plane_hypotheses_device — N = 10 images per problem, 8 iterations,
 photometric then geometric, the pass order of src/main_ACMMP.cpp:123-137 and
-one RunPatchMatch per view (src/ACMMP.cu:1378-1456).
+one RunPatchMatch per view (src/ACMMP.cu:1378-1456), each view with the
+bench's own Philox key (bench.VIEW_SEED + view id).
 
 Every view's planes (world normal + depth) and costs after each pass are
 compared BIT-EXACTLY with the CPU oracle run on the same inputs and the
@@ -22,6 +23,8 @@ import torch
 import oracle
 from acmmp_amd import default_params, scene
 from acmmp_amd.resident import EnginePool, ResidentViews
+
+import bench  # the bench's per-view Philox keys (conftest puts the repo root on sys.path)
 from parity_util import assert_bit_exact
 
 pytestmark = pytest.mark.gpu
@@ -35,7 +38,7 @@ def _cfg2(width, height, views=10, nsrc=9, iters=8, streams=2):
     srcs = {k: setup.pairs[k][:nsrc] for k in range(views)}
     torch.cuda.synchronize()
     pool = EnginePool(0, streams)
-    rv = ResidentViews(pool, cams, images, srcs, range(views), height, width)
+    rv = ResidentViews(pool, cams, images, srcs, range(views), height, width, view_seed=bench.VIEW_SEED)
     photo = default_params()
     photo.max_iterations = iters
     geom = default_params()
