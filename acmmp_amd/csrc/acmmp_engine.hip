@@ -324,25 +324,6 @@ int kv_upload(acmmp_ctx *ctx) {
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
     kv.texel = ctx->pad_texel;
-    // lane views: one uniform base below every source view's u8 records,
-    // 32-bit byte offsets from it (KViews::lv_ok)
-    kv.lv_ok = 0;
-    kv.lv_base = nullptr;
-    if (kv.texel == kTexelU8 && !kv.wide && ctx->n >= 2) {
-        uintptr_t lo = UINTPTR_MAX, hi = 0;
-        for (int i = 1; i < ctx->n; ++i) {
-            const uintptr_t a = (uintptr_t)ctx->pad_use[i];
-            lo = std::min(lo, a);
-            hi = std::max(hi, a + (uintptr_t)4 * ctx->pad_pitch[i] * (ctx->cams[i].height + 2));
-        }
-        const char *e = std::getenv("ACMMP_LANE_VIEWS");
-        const bool on = !(e && e[0] == '0');
-        if (on && hi - lo < ((uintptr_t)1 << 32)) {
-            kv.lv_ok = 1;
-            kv.lv_base = (const unsigned char *)lo;
-            for (int i = 1; i < ctx->n; ++i) kv.lv_off[i] = (uint32_t)((uintptr_t)ctx->pad_use[i] - lo);
-        }
-    }
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737

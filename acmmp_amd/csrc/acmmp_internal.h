@@ -66,14 +66,6 @@ struct KViews {
     int texel;                                // form of pad[]: kTexelF32 / kTexelU8 / kTexelH16
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
-    // Lane views (k_sweep's packed current-plane and refinement evaluations,
-    // where the source view differs across a wave's lanes): u8-quad records
-    // of source v at lv_base + lv_off[v] + 4 * record. lv_ok: u8 form, fp32
-    // record indices, every source view's records within 4 GiB of lv_base
-    // (else, or with ACMMP_LANE_VIEWS=0, the per-view loops run instead).
-    const unsigned char *lv_base;
-    uint32_t lv_off[ACMMP_MAX_IMAGES];
-    int lv_ok;
 };
 
 struct KState {

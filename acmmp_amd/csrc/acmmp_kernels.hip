@@ -28,7 +28,6 @@
 namespace acmmp {
 
 #define DEV static __device__ __forceinline__
-#define MDEV __device__ __forceinline__  // member functions
 
 // Patch geometry fixed by the reference defaults (patch_size 11, increment 2:
 // offsets {-5,-3,-1,1,3,5}^2, src/ACMMP.h:34,37). The engine rejects others.
@@ -50,32 +49,6 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
-// Timing-only upper bounds (A/B builds only, wrong results): the current
-// plane's NCC calls skipped (its stored cost stands in), or the refinement's.
-#ifndef ACMMP_UB_SKIP_NOW
-#define ACMMP_UB_SKIP_NOW 0
-#endif
-#ifndef ACMMP_UB_SKIP_REFINE
-#define ACMMP_UB_SKIP_REFINE 0
-#endif
-// (bounds on the refinement's packing, all with its results discarded so no
-// refinement plane is ever accepted and the downstream work is the same:
-// DISCARD alone = the product's evaluation; ALWAYS_FAST = every NCC takes the
-// Newton-reciprocal path; XVIEW_PACK = the items of all views packed into
-// full-wave passes as if they were one view's, i.e. ideal cross-view packing)
-// cost_array columns only for views that can be sampled (A/B: 0 = one per view)
-#ifndef ACMMP_COST_SLOTS
-#define ACMMP_COST_SLOTS 1
-#endif
-#ifndef ACMMP_UB_REFINE_DISCARD
-#define ACMMP_UB_REFINE_DISCARD 0
-#endif
-#ifndef ACMMP_UB_ALWAYS_FAST
-#define ACMMP_UB_ALWAYS_FAST 0
-#endif
-#ifndef ACMMP_UB_XVIEW_PACK
-#define ACMMP_UB_XVIEW_PACK 0
-#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -233,23 +206,22 @@ DEV float4 perturbed_normal(const acmmp_camera &c, int px, int py, float4 normal
 
 // ------------------------------------------------------ homography + NCC
 // ComputeHomography (src/ACMMP.cu:262-322) with the camera-only terms
-// precomputed per view (ViewRel) and pin P4. VS provides the source view's
-// Rr(i), tr(i) (ViewRel) and K(i): from KViews with a wave-uniform view
-// (scalar loads), or from the LDS LaneView table with a per-lane view.
-template <class VS>
-DEV void homography_g(const KViews &kv, const VS &src, float4 h, float *H) {
+// precomputed per view (ViewRel) and pin P4.
+DEV void homography(const KViews &kv, int v, float4 h, float *H) {
+    const ViewRel &r = kv.rel[v];
     const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
     const float inv_w = 1.0f / h.w;
     float G[9];
-    G[0] = src.Rr(0) - (src.tr(0) * h.x) * inv_w;
-    G[1] = src.Rr(1) - (src.tr(0) * h.y) * inv_w;
-    G[2] = src.Rr(2) - (src.tr(0) * h.z) * inv_w;
-    G[3] = src.Rr(3) - (src.tr(1) * h.x) * inv_w;
-    G[4] = src.Rr(4) - (src.tr(1) * h.y) * inv_w;
-    G[5] = src.Rr(5) - (src.tr(1) * h.z) * inv_w;
-    G[6] = src.Rr(6) - (src.tr(2) * h.x) * inv_w;
-    G[7] = src.Rr(7) - (src.tr(2) * h.y) * inv_w;
-    G[8] = src.Rr(8) - (src.tr(2) * h.z) * inv_w;
+    G[0] = r.Rr[0] - (r.tr[0] * h.x) * inv_w;
+    G[1] = r.Rr[1] - (r.tr[0] * h.y) * inv_w;
+    G[2] = r.Rr[2] - (r.tr[0] * h.z) * inv_w;
+    G[3] = r.Rr[3] - (r.tr[1] * h.x) * inv_w;
+    G[4] = r.Rr[4] - (r.tr[1] * h.y) * inv_w;
+    G[5] = r.Rr[5] - (r.tr[1] * h.z) * inv_w;
+    G[6] = r.Rr[6] - (r.tr[2] * h.x) * inv_w;
+    G[7] = r.Rr[7] - (r.tr[2] * h.y) * inv_w;
+    G[8] = r.Rr[8] - (r.tr[2] * h.z) * inv_w;
     const float ik0 = kv.inv_k0, ik4 = kv.inv_k4;
     float t[9];
     t[0] = G[0] * ik0;
@@ -261,34 +233,16 @@ DEV void homography_g(const KViews &kv, const VS &src, float4 h, float *H) {
     t[6] = G[6] * ik0;
     t[7] = G[7] * ik4;
     t[8] = ((-G[6] * rc.K[2]) * ik0 - (G[7] * rc.K[5]) * ik4) + G[8];
-    H[0] = src.K(0) * t[0] + src.K(2) * t[6];
-    H[1] = src.K(0) * t[1] + src.K(2) * t[7];
-    H[2] = src.K(0) * t[2] + src.K(2) * t[8];
-    H[3] = src.K(4) * t[3] + src.K(5) * t[6];
-    H[4] = src.K(4) * t[4] + src.K(5) * t[7];
-    H[5] = src.K(4) * t[5] + src.K(5) * t[8];
-    H[6] = src.K(8) * t[6];
-    H[7] = src.K(8) * t[7];
-    H[8] = src.K(8) * t[8];
+    H[0] = sc.K[0] * t[0] + sc.K[2] * t[6];
+    H[1] = sc.K[0] * t[1] + sc.K[2] * t[7];
+    H[2] = sc.K[0] * t[2] + sc.K[2] * t[8];
+    H[3] = sc.K[4] * t[3] + sc.K[5] * t[6];
+    H[4] = sc.K[4] * t[4] + sc.K[5] * t[7];
+    H[5] = sc.K[4] * t[5] + sc.K[5] * t[8];
+    H[6] = sc.K[8] * t[6];
+    H[7] = sc.K[8] * t[7];
+    H[8] = sc.K[8] * t[8];
 }
-
-// Source view v of KViews (wave-uniform v): ViewRel, camera, depth map.
-struct UView {
-    const KViews &kv;
-    int v;
-    MDEV float Rr(int i) const { return kv.rel[v].Rr[i]; }
-    MDEV float tr(int i) const { return kv.rel[v].tr[i]; }
-    MDEV float K(int i) const { return kv.cam[v].K[i]; }
-    MDEV float R(int i) const { return kv.cam[v].R[i]; }
-    MDEV float t(int i) const { return kv.cam[v].t[i]; }
-    MDEV float cwk(int k) const { return kv.cw[v][k]; }
-    MDEV const float *dep() const { return kv.dep[v]; }
-    MDEV int dpitch() const { return kv.dpitch[v]; }
-    MDEV int dw() const { return kv.dw[v]; }
-    MDEV int dh() const { return kv.dh[v]; }
-};
-
-DEV void homography(const KViews &kv, int v, float4 h, float *H) { homography_g(kv, UView{kv, v}, h, H); }
 
 // Exactly rounded 1/z. The IEEE division sequence (v_div_scale / v_rcp /
 // 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. Inside the
@@ -360,23 +314,6 @@ DEV SrcImage src_image(const KViews &kv, int v) {
 
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// A u8-quad source view whose index differs across the lanes of a wave (the
-// packed current-plane and refinement evaluations): its records are global
-// loads at base + off + 4 * record, base wave-uniform (KViews::lv_base, all
-// source views of the problem within 4 GiB of it: KViews::lv_ok), off,
-// W, H and the pitch per lane (LaneView, LDS).
-struct SrcImageLV {
-    const unsigned char *base;
-    uint32_t off;
-    float fw, fh, fpitch, fp1;
-};
-typedef const __attribute__((address_space(1))) uint32_t gu32;
-
-DEV float img_w(const SrcImage &im) { return (float)im.W; }
-DEV float img_h(const SrcImage &im) { return (float)im.H; }
-DEV float img_w(const SrcImageLV &im) { return im.fw; }
-DEV float img_h(const SrcImageLV &im) { return im.fh; }
 
 // ---------------------------------------------------------- ref-image tile
 // A block covers kBX colour-split columns (k0..k0+kBX-1) x kBY rows of ONE
@@ -541,14 +478,12 @@ struct RowFetch {
 
 // Projection, clamp, fractions and record index of patch row jj, and its 6
 // loads issued (not waited for).
-template <bool FAST, int TX, class IM>
-DEV void fetch_row(const IM &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
+template <bool FAST, int TX>
+DEV void fetch_row(const SrcImage &im, const float *H, const f2v *cx, const f2v *cy, const f2v *cz, int py, int jj,
                    RowFetch<TX> &rf) {
     constexpr bool WIDE = (TX & kTxWide) != 0, U8 = (TX & kTxU8) != 0, H16 = (TX & kTxH16) != 0;
     constexpr bool F8 = (TX & kTxFrac8) != 0;
-    constexpr bool LV = __is_same(IM, SrcImageLV);
-    static_assert(!LV || (U8 && !WIDE && !H16), "lane views: u8 quads with fp32 record indices only");
-    const f2v fw = splat(img_w(im)), fh = splat(img_h(im));
+    const f2v fw = splat((float)im.W), fh = splat((float)im.H);
     const f2v y = splat((float)(py - 5 + 2 * jj));
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
@@ -587,7 +522,7 @@ DEV void fetch_row(const IM &im, const float *H, const f2v *cx, const f2v *cy, c
         }
         // record index (y0 + 1) * pitch + x0 + 1
         unsigned ia, ib;
-        if constexpr (!WIDE) {
+        if (!WIDE) {
             // = fma(y0, pitch, x0 + pitch + 1): integers below 2^24, so
             // exact in fp32 (the engine selects WIDE otherwise)
             const f2v idx = fma2(fly, splat(im.fpitch), flx + im.fp1);
@@ -600,14 +535,10 @@ DEV void fetch_row(const IM &im, const float *H, const f2v *cx, const f2v *cy, c
             ia = __umul24((unsigned)r.x, (unsigned)im.pitch) + (unsigned)q.x;
             ib = __umul24((unsigned)r.y, (unsigned)im.pitch) + (unsigned)q.y;
         }
-        if constexpr (LV) {
-            // 32-bit byte offset from the uniform base: global_load saddr form
-            rf.q[2 * p] = *(gu32 *)(im.base + (uint32_t)(im.off + 4u * ia));
-            rf.q[2 * p + 1] = *(gu32 *)(im.base + (uint32_t)(im.off + 4u * ib));
-        } else if constexpr (H16) {
+        if (H16) {
             rf.hq[2 * p] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ia, 0, 0, 0);
             rf.hq[2 * p + 1] = amdgcn_struct_buffer_load_b64(im.rsrc, (int)ib, 0, 0, 0);
-        } else if constexpr (U8) {
+        } else if (U8) {
             rf.q[2 * p] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ia, 0, 0, 0);
             rf.q[2 * p + 1] = amdgcn_struct_buffer_load_b32(im.rsrc, (int)ib, 0, 0, 0);
         } else {
@@ -683,8 +614,8 @@ DEV void reduce_row(const RowFetch<TX> &rf, const WSlot *wl, const float *rt, in
 // (src/ACMMP.cu:382-412). The row loop is software-pipelined: row jj + 1's
 // loads are issued before row jj is reduced, so a row's gather latency
 // overlaps the previous row's arithmetic.
-template <bool FAST, int TX, class IM>
-DEV void ncc_sums_rows(const IM &im, const float *H, const WSlot *wl, const float *rt, int wstride, int px,
+template <bool FAST, int TX>
+DEV void ncc_sums_rows(const SrcImage &im, const float *H, const WSlot *wl, const float *rt, int wstride, int px,
                        int py, float &sum_src, float &sum_ss, float &sum_rs) {
     f2v cx[kPairs], cy[kPairs], cz[kPairs];
 #pragma unroll
@@ -699,12 +630,12 @@ DEV void ncc_sums_rows(const IM &im, const float *H, const WSlot *wl, const floa
     for (int p = 0; p < kPairs; ++p) acc_s[p] = acc_ss[p] = acc_rs[p] = splat(0.0f);
     // two rows per trip (ping-pong fetch buffers, no register copies)
     RowFetch<TX> ra, rb;
-    fetch_row<FAST, TX, IM>(im, H, cx, cy, cz, py, 0, ra);
+    fetch_row<FAST, TX>(im, H, cx, cy, cz, py, 0, ra);
 #pragma unroll 1
     for (int jj = 0; jj < kTaps; jj += 2) {
-        fetch_row<FAST, TX, IM>(im, H, cx, cy, cz, py, jj + 1, rb);
+        fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 1, rb);
         reduce_row<TX>(ra, wl, rt, wstride, jj, acc_s, acc_ss, acc_rs);
-        if (jj + 2 < kTaps) fetch_row<FAST, TX, IM>(im, H, cx, cy, cz, py, jj + 2, ra);
+        if (jj + 2 < kTaps) fetch_row<FAST, TX>(im, H, cx, cy, cz, py, jj + 2, ra);
         reduce_row<TX>(rb, wl, rt, wstride, jj + 1, acc_s, acc_ss, acc_rs);
     }
     sum_src = 0.0f;
@@ -723,8 +654,8 @@ DEV void ncc_sums_rows(const IM &im, const float *H, const WSlot *wl, const floa
 
 // Source-sample reduction of ComputeBilateralNCC (src/ACMMP.cu:382-412):
 // returns the three weighted sums (ncc_sums_rows above).
-template <bool FAST, int TX, class IM>
-DEV void ncc_sums(const IM &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
+template <bool FAST, int TX>
+DEV void ncc_sums(const SrcImage &im, const float *H, const PixPatch &pp, int px, int py, float &sum_src,
                   float &sum_ss, float &sum_rs) {
     // re-read weights from LDS each call rather than caching them in VGPRs
     // (launder the integer offset, not the pointer, so the LDS address space
@@ -732,25 +663,25 @@ DEV void ncc_sums(const IM &im, const float *H, const PixPatch &pp, int px, int 
     int wo = pp.wo;
     asm volatile("" : "+v"(wo));
     const WSlot *wl = pp.w - pp.wo + wo;
-    ncc_sums_rows<FAST, TX, IM>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
+    ncc_sums_rows<FAST, TX>(im, H, wl, pp.rt, kThreads, px, py, sum_src, sum_ss, sum_rs);
 }
 
-// ComputeBilateralNCC (src/ACMMP.cu:360-432) of plane h at pixel (px, py)
-// against one source view: VS supplies the view's homography terms, IM its
-// records. Reference samples come from the LDS tile, source samples through
-// ncc_sums.
-template <int TX, class VS, class IM>
-DEV float bilateral_ncc_g(const KViews &kv, const VS &vs, const IM &im, const PixPatch &pp, int px, int py,
-                          float4 h) {
+// ComputeBilateralNCC (src/ACMMP.cu:360-432) for source view v (1-based,
+// wave-uniform). Reference samples come from the LDS tile, source samples
+// through ncc_sums.
+template <int TX>
+DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
+                        int py, float4 h) {
     const float cost_max = 2.0f;
     const float kMinVar = 1e-5f;
     // var_ref is invariant: when it is below kMinVar (or the centre maps
     // outside the source) every call returns cost_max.
     if (pp.var < kMinVar) return cost_max;
+    const SrcImage im = src_image<TX>(kv, v);
     float H[9];
-    homography_g(kv, vs, h, H);
+    homography(kv, v, h, H);
     const float2 pt = project(H, (float)px, (float)py);
-    if (pt.x >= img_w(im) || pt.x < 0.0f || pt.y >= img_h(im) || pt.y < 0.0f) return cost_max;
+    if (pt.x >= (float)im.W || pt.x < 0.0f || pt.y >= (float)im.H || pt.y < 0.0f) return cost_max;
     float sum_src, sum_ss, sum_rs;
     // hz is affine in the sample position, so its values over the patch lie
     // between the four corner values (up to rounding: the window test uses a
@@ -763,10 +694,9 @@ DEV float bilateral_ncc_g(const KViews &kv, const VS &vs, const IM &im, const Pi
     const float z11 = dm_fma(H[7], yb, dm_fma(H[6], xr, H[8]));
     const float zmin = fminf(fminf(z00, z10), fminf(z01, z11));
     const float zmax = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
-    const bool fast = ACMMP_UB_ALWAYS_FAST ||
-                      (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
-    if (fast) ncc_sums<true, TX, IM>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
-    else ncc_sums<false, TX, IM>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    const bool fast = (zmin >= 0x1p-124f && zmax < 0x1p124f) || (zmax <= -0x1p-124f && zmin > -0x1p124f);
+    if (fast) ncc_sums<true, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
+    else ncc_sums<false, TX>(im, H, pp, px, py, sum_src, sum_ss, sum_rs);
     sum_src *= pp.inv_wsum;
     const float var_src = dm_fma(sum_ss, pp.inv_wsum, -(sum_src * sum_src));  // pin P3
     if (var_src < kMinVar) return cost_max;
@@ -776,76 +706,6 @@ DEV float bilateral_ncc_g(const KViews &kv, const VS &vs, const IM &im, const Pi
     c = (c < cost_max) ? c : cost_max;
     c = (c > 0.0f) ? c : 0.0f;
     return c;
-}
-
-// ComputeBilateralNCC for source view v (1-based, wave-uniform).
-template <int TX>
-DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPatch &pp, int v, int px,
-                        int py, float4 h) {
-    if (pp.var < 1e-5f) return 2.0f;
-    return bilateral_ncc_g<TX>(kv, UView{kv, v}, src_image<TX>(kv, v), pp, px, py, h);
-}
-
-// ------------------------------------------------------------ lane views
-// Per-source-view constants for NCC and geometric evaluations whose view
-// differs across the lanes of a wave (the packed current-plane and
-// refinement evaluations of k_sweep): staged once per block in LDS (slot j
-// = source view j + 1) and read with per-lane indices, so one wave-wide pass
-// can serve (lane, view) items of every view. Same values as KViews holds.
-struct alignas(16) LaneView {
-    float Rr[9], tr[3];          // ViewRel
-    float K[9];                  // source camera
-    float fw, fh, fpitch, fp1;   // width, height, record pitch, pitch + 1
-    uint32_t off;                // u8 records at KViews::lv_base + off
-    float R[9], t[3], cw[3];     // source camera (geometric cost), -(R^T t)
-    int dpitch, dw, dh;
-    const float *dep;            // source depth map (geometric passes)
-};
-
-struct LView {
-    const LaneView &L;
-    MDEV float Rr(int i) const { return L.Rr[i]; }
-    MDEV float tr(int i) const { return L.tr[i]; }
-    MDEV float K(int i) const { return L.K[i]; }
-    MDEV float R(int i) const { return L.R[i]; }
-    MDEV float t(int i) const { return L.t[i]; }
-    MDEV float cwk(int k) const { return L.cw[k]; }
-    MDEV const float *dep() const { return L.dep; }
-    MDEV int dpitch() const { return L.dpitch; }
-    MDEV int dw() const { return L.dw; }
-    MDEV int dh() const { return L.dh; }
-};
-
-// thread `tid` < nsrc fills slot tid (view tid + 1); the caller's
-// __syncthreads publishes the table
-DEV void fill_lane_views(const KViews &kv, LaneView *lvt, int tid) {
-    if (tid >= kv.nsrc) return;
-    const int v = tid + 1;
-    LaneView &L = lvt[tid];
-    const acmmp_camera &c = kv.cam[v];
-    for (int i = 0; i < 9; ++i) {
-        L.Rr[i] = kv.rel[v].Rr[i];
-        L.K[i] = c.K[i];
-        L.R[i] = c.R[i];
-    }
-    for (int i = 0; i < 3; ++i) {
-        L.tr[i] = kv.rel[v].tr[i];
-        L.t[i] = c.t[i];
-        L.cw[i] = kv.cw[v][i];
-    }
-    L.fw = (float)c.width;
-    L.fh = (float)c.height;
-    L.fpitch = (float)kv.ppitch[v];
-    L.fp1 = (float)(kv.ppitch[v] + 1);
-    L.off = kv.lv_off[v];
-    L.dpitch = kv.dpitch[v];
-    L.dw = kv.dw[v];
-    L.dh = kv.dh[v];
-    L.dep = kv.dep[v];
-}
-
-DEV SrcImageLV lane_image(const KViews &kv, const LaneView &L) {
-    return SrcImageLV{kv.lv_base, L.off, L.fw, L.fh, L.fpitch, L.fp1};
 }
 
 // ComputeMultiViewInitialCostandSelectedViews (src/ACMMP.cu:434-471)
@@ -928,46 +788,36 @@ struct GeomFetch {
     float sx, sy, dep;
 };
 
-// -(R^T t) of the source view, component k (cam_offset of a view accessor)
-template <class VS>
-DEV float src_offset(const VS &sc, int k) {
-#ifdef ACMMP_CUDA_NUMERICS
-    return -(sc.R(k) * sc.t(0) + sc.R(3 + k) * sc.t(1) + sc.R(6 + k) * sc.t(2));
-#else
-    return sc.cwk(k);
-#endif
-}
-
-template <class VS>
-DEV GeomFetch geom_fetch_g(const VS &sc, const GeomRef &g) {
+DEV GeomFetch geom_fetch(const KViews &kv, int v, const GeomRef &g) {
+    const acmmp_camera &sc = kv.cam[v];
     const float *Wp = g.Wp;
     // ProjectonCamera_cu (:506-516)
     float T[3];
-    T[0] = sc.R(0) * Wp[0] + sc.R(1) * Wp[1] + sc.R(2) * Wp[2] + sc.t(0);
-    T[1] = sc.R(3) * Wp[0] + sc.R(4) * Wp[1] + sc.R(5) * Wp[2] + sc.t(1);
-    T[2] = sc.R(6) * Wp[0] + sc.R(7) * Wp[1] + sc.R(8) * Wp[2] + sc.t(2);
-    const float sd = sc.K(6) * T[0] + sc.K(7) * T[1] + sc.K(8) * T[2];
+    T[0] = sc.R[0] * Wp[0] + sc.R[1] * Wp[1] + sc.R[2] * Wp[2] + sc.t[0];
+    T[1] = sc.R[3] * Wp[0] + sc.R[4] * Wp[1] + sc.R[5] * Wp[2] + sc.t[1];
+    T[2] = sc.R[6] * Wp[0] + sc.R[7] * Wp[1] + sc.R[8] * Wp[2] + sc.t[2];
+    const float sd = sc.K[6] * T[0] + sc.K[7] * T[1] + sc.K[8] * T[2];
     GeomFetch f;
-    f.sx = (sc.K(0) * T[0] + sc.K(1) * T[1] + sc.K(2) * T[2]) / sd;
-    f.sy = (sc.K(3) * T[0] + sc.K(4) * T[1] + sc.K(5) * T[2]) / sd;
-    f.dep = tex_trunc(sc.dep(), sc.dpitch(), sc.dw(), sc.dh(), f.sx, f.sy);
+    f.sx = (sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2]) / sd;
+    f.sy = (sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2]) / sd;
+    f.dep = tex_trunc(kv.dep[v], kv.dpitch[v], kv.dw[v], kv.dh[v], f.sx, f.sy);
     return f;
 }
 
-template <class VS>
-DEV float geom_finish_g(const KViews &kv, const VS &sc, const GeomFetch &f, int px, int py) {
+DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int py) {
     const float max_cost = 3.0f;
     const acmmp_camera &rc = kv.cam[0];
+    const acmmp_camera &sc = kv.cam[v];
     const float sx = f.sx, sy = f.sy, src_depth = f.dep;
     if (src_depth == 0.0f) return max_cost;
     float Y[3];
-    Y[0] = src_depth * (sx - sc.K(2)) / sc.K(0);
-    Y[1] = src_depth * (sy - sc.K(5)) / sc.K(4);
+    Y[0] = src_depth * (sx - sc.K[2]) / sc.K[0];
+    Y[1] = src_depth * (sy - sc.K[5]) / sc.K[4];
     Y[2] = src_depth;
     float Wq[3];
-    Wq[0] = (sc.R(0) * Y[0] + sc.R(3) * Y[1] + sc.R(6) * Y[2]) + src_offset(sc, 0);
-    Wq[1] = (sc.R(1) * Y[0] + sc.R(4) * Y[1] + sc.R(7) * Y[2]) + src_offset(sc, 1);
-    Wq[2] = (sc.R(2) * Y[0] + sc.R(5) * Y[1] + sc.R(8) * Y[2]) + src_offset(sc, 2);
+    Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) + cam_offset(kv, v, 0);
+    Wq[1] = (sc.R[1] * Y[0] + sc.R[4] * Y[1] + sc.R[7] * Y[2]) + cam_offset(kv, v, 1);
+    Wq[2] = (sc.R[2] * Y[0] + sc.R[5] * Y[1] + sc.R[8] * Y[2]) + cam_offset(kv, v, 2);
     float U[3];
     U[0] = rc.R[0] * Wq[0] + rc.R[1] * Wq[1] + rc.R[2] * Wq[2] + rc.t[0];
     U[1] = rc.R[3] * Wq[0] + rc.R[4] * Wq[1] + rc.R[5] * Wq[2] + rc.t[1];
@@ -979,12 +829,6 @@ DEV float geom_finish_g(const KViews &kv, const VS &sc, const GeomFetch &f, int 
     const float dr = (float)py - by;
     const float e = dm_sqrt(dc * dc + dr * dr);
     return (e < max_cost) ? e : max_cost;
-}
-
-DEV GeomFetch geom_fetch(const KViews &kv, int v, const GeomRef &g) { return geom_fetch_g(UView{kv, v}, g); }
-
-DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int py) {
-    return geom_finish_g(kv, UView{kv, v}, f, px, py);
 }
 
 DEV float geom_cost_at(const KViews &kv, int v, const GeomRef &g, int px, int py) {
@@ -1127,14 +971,8 @@ DEV LaneGeom lane_geom(int colour, BlockXY b) { return lane_geom_of(colour, b, t
 // ------------------------------------------------------------------ init
 // RandomInitialization (src/ACMMP.cu:609-705). Reads the row-major state,
 // writes the colour-split "current" buffers. blockIdx.z = colour.
-// waves per SIMD k_init is compiled for (its random-plane gathers are
-// latency-bound: more waves in flight hide more of it; A/B: DESIGN §5)
-#ifndef ACMMP_INIT_WAVES
-#define ACMMP_INIT_WAVES 2
-#endif
 template <int NS, int TX>
-__global__ __launch_bounds__(ACMMP_BLOCK_THREADS, ACMMP_INIT_WAVES) void k_init(const KViews *__restrict__ kvp,
-                                                                                KState st) {
+__global__ __launch_bounds__(ACMMP_BLOCK_THREADS) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     const KViews &kv = *kvp;
@@ -1242,185 +1080,6 @@ DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ------------------------------------------- packed lane-view evaluations
-// The current plane's costs (:1080-1092) and the 5 refinement planes' costs
-// (:743-783) need one NCC (+ geometric cost) per (lane, SAMPLED view) item.
-// Evaluated one view at a time, a view costs a whole wave pass however few
-// lanes sampled it; with lane views (LaneView, SrcImageLV) a pass serves
-// items of any views, so the wave packs all its items into ceil(items / 64)
-// passes. Items are ordered by view, then (refinement) plane, then owner
-// lane, so neighbouring lanes evaluate neighbouring pixels on one view (the
-// gathers stay coherent); an executor lane takes its owner's pixel, patch
-// weights (LDS), patch statistics and plane, and leaves the result in resb;
-// each owner then adds its results in ascending view order, exactly the
-// loop `for j: if (w_j > 0) tc += w_j * (NCC_j [+ 0.2 geom_j])` it replaces
-// (same operations, same order per owner).
-//
-// Per-wave view table: vt[j] = (first item of view j, lanes sampling j,
-// their ballot mask lo, hi); vt[nsrc] = (number of items, 0, 0, 0). Every
-// active lane writes the same (uniform) entries. Returns the item count.
-DEV int lv_view_table(uint4 *vt, uint32_t smask, int nsrc) {
-    int off = 0;
-    for (int j = 0; j < nsrc; ++j) {
-        const uint64_t m = __ballot((smask >> j) & 1u);
-        const int c = __popcll(m);
-        vt[j] = make_uint4((uint32_t)off, (uint32_t)c, (uint32_t)m, (uint32_t)(m >> 32));
-        off += c;
-    }
-    vt[nsrc] = make_uint4((uint32_t)off, 0u, 0u, 0u);
-    return off;
-}
-
-// lane index of the r-th (0-based) set bit of the 64-bit mask (lo, hi)
-DEV int nth_set_bit(uint32_t lo, uint32_t hi, int r) {
-    int pos = 0;
-    uint32_t m = lo;
-    const int cl = __popc(lo);
-    if (r >= cl) {
-        r -= cl;
-        m = hi;
-        pos = 32;
-    }
-    int c = __popc(m & 0xffffu);
-    if (r >= c) { r -= c; m >>= 16; pos += 16; }
-    c = __popc(m & 0xffu);
-    if (r >= c) { r -= c; m >>= 8; pos += 8; }
-    c = __popc(m & 0xfu);
-    if (r >= c) { r -= c; m >>= 4; pos += 4; }
-    c = __popc(m & 0x3u);
-    if (r >= c) { r -= c; m >>= 2; pos += 2; }
-    if (r >= (int)(m & 1u)) pos += 1;
-    return pos;
-}
-
-// One (owner, view) item: NCC of plane h at the owner's pixel against lane
-// view L, plus 0.2 x the geometric cost in geometric passes (depth fetch
-// issued ahead of the NCC's gathers).
-template <int TX>
-DEV float lv_item(const KViews &kv, const LaneView &L, const PixPatch &op, const LaneGeom &og, float4 h) {
-    GeomFetch gf = {};
-    if (kv.prm.geom_consistency) gf = geom_fetch_g(LView{L}, geom_ref(kv, h, og.px, og.py));
-    const float c = bilateral_ncc_g<TX>(kv, LView{L}, lane_image(kv, L), op, og.px, og.py, h);
-    return kv.prm.geom_consistency ? c + 0.2f * geom_finish_g(kv, LView{L}, gf, og.px, og.py) : c;
-}
-
-// sum_j w_j * (NCC_j [+ 0.2 geom_j]) of the current plane over the lane's
-// sampled views (smask), j ascending (:1083-1089); n = the wave's items.
-template <int TX>
-DEV float current_cost_packed(const KViews &kv, const LaneView *lvt, const uint4 *vt, float *resb,
-                              const float *tile, WSlot *wlds, const PixPatch &pp, float4 my_plane,
-                              const ViewCounts &vw, uint32_t smask, int n, int colour, BlockXY blk) {
-    const int tid = pp.wo, lane = tid & 63, wbase = tid & ~63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t act = __ballot(1);
-    const int nact = __popcll(act), arank = __popcll(act & lt);
-    float tc = 0.0f;
-    uint32_t rem = smask;
-    int jb = 0;
-    for (int base = 0; base < n; base += nact) {
-        const int k = base + arank;
-        while ((int)vt[jb + 1].x <= base) ++jb;  // the view of the pass's first item
-        int j = jb, o = lane;
-        if (k < n) {
-            while ((int)vt[j + 1].x <= k) ++j;
-            const uint4 e = vt[j];
-            o = nth_set_bit(e.z, e.w, k - (int)e.x);
-        }
-        // the owner's plane and patch statistics (every active lane takes part)
-        const float4 h = make_float4(__shfl(my_plane.x, o), __shfl(my_plane.y, o), __shfl(my_plane.z, o),
-                                     __shfl(my_plane.w, o));
-        PixPatch op;
-        op.mean = __shfl(pp.mean, o);
-        op.var = __shfl(pp.var, o);
-        op.inv_wsum = __shfl(pp.inv_wsum, o);
-        if (k < n) {
-            const int otid = wbase + o;
-            const LaneGeom og = lane_geom_of(colour, blk, otid);
-            op.wo = otid;
-            op.w = wlds + otid;
-            op.rt = tile + og.tb;
-            resb[wbase + arank] = lv_item<TX>(kv, lvt[j], op, og, h);
-        }
-        wave_sync();
-        // the owner adds its items of this pass, views ascending
-        const int end = base + nact;
-        while (rem) {
-            const int jj = __ffs(rem) - 1;
-            const uint4 e = vt[jj];
-            const int kk = (int)e.x + __popcll((((uint64_t)e.w << 32) | e.z) & lt);
-            if (kk >= end) break;
-            const float wj = (float)vw.get(jj);
-            tc += wj * resb[wbase + (kk - base)];
-            rem &= rem - 1u;
-        }
-        wave_sync();
-    }
-    return tc;
-}
-
-// The 5 refinement planes' sums (refine_costs_compact's result), items
-// ordered by view j, plane t, owner: item k of view j is plane
-// t = (k - 5 off_j) / c_j of the owner of rank (k - 5 off_j) mod c_j.
-template <int TX>
-DEV void refine_costs_packed(const KViews &kv, const LaneView *lvt, const uint4 *vt, float *resb,
-                             const float *tile, WSlot *wlds, float4 *lds, const ViewCounts &vw, uint32_t smask,
-                             int n, int colour, BlockXY blk, int tid) {
-    const int lane = tid & 63, wbase = tid & ~63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t act = __ballot(1);
-    const int nact = __popcll(act), arank = __popcll(act & lt);
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f, a4 = 0.0f;
-    uint32_t rem = smask;
-    int tcur = 0, jb = 0;
-    const int n5 = 5 * n;
-    for (int base = 0; base < n5; base += nact) {
-        const int k = base + arank;
-        while (5 * (int)vt[jb + 1].x <= base) ++jb;
-        if (k < n5) {
-            int j = jb;
-            while (5 * (int)vt[j + 1].x <= k) ++j;
-            const uint4 e = vt[j];
-            const int q = k - 5 * (int)e.x, c = (int)e.y;
-            const int t = (q >= c) + (q >= 2 * c) + (q >= 3 * c) + (q >= 4 * c);
-            const int otid = wbase + nth_set_bit(e.z, e.w, q - t * c);
-            const LaneGeom og = lane_geom_of(colour, blk, otid);
-            PixPatch op;
-            op.wo = otid;
-            op.w = wlds + otid;
-            op.rt = tile + og.tb;
-            op.mean = cmp_pd(lds, 1, otid);
-            op.var = cmp_pd(lds, 2, otid);
-            op.inv_wsum = cmp_pd(lds, 3, otid);
-            resb[wbase + arank] = lv_item<TX>(kv, lvt[j], op, og, lds[t * kThreads + otid]);
-        }
-        wave_sync();
-        const int end = base + nact;
-        while (rem) {
-            const int jj = __ffs(rem) - 1;
-            const uint4 e = vt[jj];
-            const int kk = 5 * (int)e.x + tcur * (int)e.y + __popcll((((uint64_t)e.w << 32) | e.z) & lt);
-            if (kk >= end) break;
-            const float r = (float)vw.get(jj) * resb[wbase + (kk - base)];
-            a0 = tcur == 0 ? a0 + r : a0;
-            a1 = tcur == 1 ? a1 + r : a1;
-            a2 = tcur == 2 ? a2 + r : a2;
-            a3 = tcur == 3 ? a3 + r : a3;
-            a4 = tcur == 4 ? a4 + r : a4;
-            if (++tcur == 5) {
-                tcur = 0;
-                rem &= rem - 1u;
-            }
-        }
-        wave_sync();
-    }
-    cmp_res(lds, 0, tid) = a0;
-    cmp_res(lds, 1, tid) = a1;
-    cmp_res(lds, 2, tid) = a2;
-    cmp_res(lds, 3, tid) = a3;
-    cmp_res(lds, 4, tid) = a4;
-    wave_sync();
-}
-
 // The 5 refinement hypotheses of PlaneHypothesisRefinement (src/ACMMP.cu:
 // 743-783) cost sum_j w_j * (NCC_j (+ 0.2 geom_j)) over the lane's sampled
 // views j. Their planes are fixed before any of them is evaluated, so all 5
@@ -1435,8 +1094,7 @@ DEV void refine_costs_packed(const KViews &kv, const LaneView *lvt, const uint4 
 template <int TX, typename RD, typename RN>
 DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, float4 *lds, const PixPatch &pp,
                               const ViewCounts &vw, int nsrc, int colour, BlockXY blk, RD ref_depth,
-                              RN ref_normal, int px, int py, const LaneView *lvt, const uint4 *vt, float *resb,
-                              uint32_t smask, int nitems) {
+                              RN ref_normal, int px, int py) {
     const acmmp_camera &c0 = kv.cam[0];
     const int tid = pp.wo;
 #pragma unroll
@@ -1452,44 +1110,9 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint64_t act = __ballot(1);
     const int nact = __popcll(act), arank = __popcll(act & lt);
-    wave_sync();
-    constexpr bool kLVForm = (TX & kTxU8) && !(TX & kTxWide) && !(TX & kTxH16);
-    if constexpr (kLVForm) {
-        if (kv.lv_ok) {  // every view's items packed together (refine_costs_packed)
-            refine_costs_packed<TX>(kv, lvt, vt, resb, tile, wlds, lds, vw, smask, nitems, colour, blk, tid);
-            return;
-        }
-    }
     float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    if (ACMMP_UB_XVIEW_PACK) {
-        int total = 0;
-        for (int j = 0; j < nsrc; ++j) total += __popcll(__ballot(vw.get(j) > 0));
-        cmp_list(lds, wbase + arank) = lane;
-        wave_sync();
-        const int n = 5 * total;
-        for (int base = 0; base < n; base += nact) {
-            const int k = base + arank;
-            if (k < n) {
-                const int t = k % 5;
-                const int otid = wbase + cmp_list(lds, wbase + (k / 5) % nact);
-                const LaneGeom og = lane_geom_of(colour, blk, otid);
-                PixPatch op;
-                op.wo = otid;
-                op.w = wlds + otid;
-                op.rt = tile + og.tb;
-                op.mean = cmp_pd(lds, 1, otid);
-                op.var = cmp_pd(lds, 2, otid);
-                op.inv_wsum = cmp_pd(lds, 3, otid);
-                const float4 h = lds[t * kThreads + otid];
-                GeomFetch gf = {};
-                if (kv.prm.geom_consistency) gf = geom_fetch(kv, 1, geom_ref(kv, h, og.px, og.py));
-                const float cc = bilateral_ncc<TX>(kv, tile, og.tb, op, 1, og.px, og.py, h);
-                cmp_res(lds, t, otid) = kv.prm.geom_consistency ? cc + 0.2f * geom_finish(kv, 1, gf, og.px, og.py) : cc;
-            }
-        }
-        wave_sync();
-    }
-    for (int j = 0; j < nsrc && !ACMMP_UB_XVIEW_PACK; ++j) {
+    wave_sync();
+    for (int j = 0; j < nsrc; ++j) {
         const float wj = (float)vw.get(j);
         const uint64_t m = __ballot(wj > 0);
         if (m == 0) continue;
@@ -1499,7 +1122,7 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
         const int n = 5 * c;
         for (int base = 0; base < n; base += nact) {
             const int k = base + arank;
-            if (k < n && !ACMMP_UB_SKIP_REFINE) {
+            if (k < n) {
                 const int t = k / c;
                 const int otid = wbase + cmp_list(lds, wbase + (k - t * c));
                 const LaneGeom og = lane_geom_of(colour, blk, otid);
@@ -1528,16 +1151,9 @@ DEV void refine_costs_compact(const KViews &kv, const float *tile, WSlot *wlds, 
         wave_sync();
         if (wj > 0) {
 #pragma unroll
-            for (int t = 0; t < 5; ++t)
-                acc[t] += wj * ((ACMMP_UB_SKIP_REFINE || ACMMP_UB_REFINE_DISCARD) ? 2.0f : cmp_res(lds, t, tid));
+            for (int t = 0; t < 5; ++t) acc[t] += wj * cmp_res(lds, t, tid);
         }
         wave_sync();
-    }
-    if (ACMMP_UB_XVIEW_PACK) {
-        float wn = 0.0f;
-        for (int j = 0; j < nsrc; ++j) wn += (float)vw.get(j);
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc[t] = 2.0f * wn;
     }
 #pragma unroll
     for (int t = 0; t < 5; ++t) cmp_res(lds, t, tid) = acc[t];
@@ -1555,19 +1171,9 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     __shared__ float4 cand_lds[8 * kThreads];
-    // lane views (u8 records, fp32 indices): the per-view table, the
-    // per-wave item tables and the pass results of the packed evaluations
-    constexpr bool kLVForm = (TX & kTxU8) && !(TX & kTxWide) && !(TX & kTxH16);
-    constexpr int kLV = kLVForm ? NS : 1;
-    __shared__ LaneView lvt[kLV];
-    __shared__ uint4 vtab[kThreads / 64][kLV + 1];
-    __shared__ float resb[kLVForm ? kThreads : 1];
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block(st.y0 / kBY);
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
-    if constexpr (kLVForm) {
-        if (kv.lv_ok) fill_lane_views(kv, lvt, threadIdx.y * kBX + threadIdx.x);
-    }
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
     const int px = g.px, py = g.py;
@@ -1700,19 +1306,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
-    // Column slots: the 8 x NS matrix only feeds final_costs of the SAMPLED
-    // views, and a view whose sampling probability is exactly 0 is never
-    // sampled (its CDF entry equals its predecessor's, so the reference's
-    // "first i with cdf[i] > r" never lands on it), view 0 excepted (cdf[0]
-    // = 0 > r for r = u - FLT_EPSILON < 0). So view v's 8 costs are written
-    // to the next free column, which advances only if v may be sampled by
-    // some lane of the wave (wave-uniform, so the scratch stores stay
-    // coalesced): a view no lane can sample has its column overwritten by the
-    // next view while its lines are still in L2. Column of view j:
-    // popcount(stored below j), stored wave-uniform.
-    uint32_t stored = 0;
-    int ncol = 0;
-    auto col_of = [&](int j) -> int { return ACMMP_COST_SLOTS ? __popc(stored & ((1u << j) - 1u)) : j; };
     // view-selection inputs (:994-1032), folded into the view-major candidate
     // loop so each view's 8 costs are consumed from registers
     float probs[NS];
@@ -1740,7 +1333,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             float c;
             if ((flags >> d) & 1u) c = bilateral_ncc<TX>(kv, tile, g.tb, pp, v + 1, px, py, cand(d));
             else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
-            cost_array[d][ACMMP_COST_SLOTS ? ncol : v] = c;
+            cost_array[d][v] = c;
             if (c < cost_threshold) {
                 tmpw += dm_expf(c * c / (-0.18f));
                 count++;
@@ -1754,10 +1347,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         if (count > 2 && count_false < 3) pr = tmpw / count;
         else if (count_false < 3) pr = dm_expf(cost_threshold * cost_threshold / (-0.32f));
         probs[v] = pr * vsp;
-        if (__ballot(v == 0 || probs[v] != 0.0f) != 0) {
-            stored |= 1u << v;
-            ++ncol;
-        }
     }
 
     // ---- multi-hypothesis joint view selection (:994-1056)
@@ -1803,12 +1392,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         const int c = vw.get(i);
         if (c > 0) { temp_sv |= (1u << i); weight_norm += (float)c; }
     }
-    // the wave's (lane, sampled view) items for the packed evaluations
-    int nitems = 0;
-    uint4 *vt = vtab[(threadIdx.y * kBX + threadIdx.x) >> 6];
-    if constexpr (kLVForm) {
-        if (kv.lv_ok) nitems = lv_view_table(vt, temp_sv, nsrc);
-    }
     float final_costs[8];
     if (!prm.geom_consistency) {
         // photometric: the NS cost loads of a candidate issued together
@@ -1820,7 +1403,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             for (int j = 0; j < NS; ++j)
                 if (j < nsrc) {
                     const float wj = (float)vw.get(j);
-                    fc += wj > 0 ? wj * cost_array[i][col_of(j)] : 0.0f;
+                    fc += wj > 0 ? wj * cost_array[i][j] : 0.0f;
                 }
             final_costs[i] = fc / weight_norm;
         }
@@ -1846,7 +1429,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             // batch of scratch loads, not one load and wait per sampled view)
             float ci[NS];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) ci[j] = j < nsrc ? cost_array[i][col_of(j)] : 0.0f;
+            for (int j = 0; j < NS; ++j) ci[j] = j < nsrc ? cost_array[i][j] : 0.0f;
             if (fl) {
                 // views no lane of the wave sampled add +0 for every lane:
                 // their geometric cost is not finished (wave-uniform skip;
@@ -1882,11 +1465,11 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             const float wj = (float)vw.get(j);
             if (wj > 0) {
                 if (prm.geom_consistency) {
-                    const float cij = cost_array[i][col_of(j)];
+                    const float cij = cost_array[i][j];
                     if (fl) fc += wj * (cij + 0.2f * geom_cost_at(kv, j + 1, gi, px, py));
                     else fc += wj * (cij + 0.1f * 3.0f);
                 } else {
-                    fc += wj * cost_array[i][col_of(j)];
+                    fc += wj * cost_array[i][j];
                 }
             }
         }
@@ -1928,7 +1511,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         // all 5 refinement costs at once (their planes go to LDS slots 0..4)
         if (t == 1)
             refine_costs_compact<TX>(kv, tile, wlds, cand_lds, pp, vw, nsrc, colour, blk, ref_depth, ref_normal,
-                                     px, py, lvt, vt, resb, temp_sv, nitems);
+                                     px, py);
         float4 h;
         if (t == 0) h = my_plane;
         else h = cand_lds[(t - 1) * kThreads + pp.wo];  // stored by refine_costs_compact
@@ -1937,11 +1520,6 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
         float tc = 0.0f;
         if (t >= 1) {
             tc = cmp_res(cand_lds, t - 1, pp.wo);
-        } else if (ACMMP_UB_SKIP_NOW) {
-            tc = my_cost * weight_norm;  // timing-only bound: the stored cost stands in (wrong results)
-        } else if (kLVForm && kv.lv_ok) {
-            if constexpr (kLVForm)
-                tc = current_cost_packed<TX>(kv, lvt, vt, resb, tile, wlds, pp, h, vw, temp_sv, nitems, colour, blk);
         } else {
         GeomRef gnow = {};
         if (prm.geom_consistency) gnow = geom_ref(kv, h, px, py);  // once for the current plane

@@ -9,7 +9,7 @@ notice losing them:
   condition is sunk into its block and waited alone: one latency per step);
 - no resource regression: 2 waves/SIMD for every source-count bucket (NS 9,
   16, 20, 32), scratch no larger than recorded per bucket, LDS within two
-  blocks per CU (the lane-view tables grow with NS).
+  blocks per CU.
 The search-cost check reads a scheduling depth (the deepest vmcnt wait), a
 property of this compiler's schedule, not of the source: it runs only under
 the hipcc it was tuned on (ROCm 7.2.0) and must be re-tuned on an upgrade.
@@ -67,9 +67,8 @@ def test_search_costs_in_flight_together(listing):
     assert max(depths) >= 60, max(depths)
 
 
-# scratch per lane of each bucket (cost_array[8][NS] dominates): round 5's,
-# NS 9 +16 B with round 6's packed lane-view evaluations
-SCRATCH_MAX = {9: 400, 16: 672, 20: 816, 32: 1264}
+# scratch per lane of each bucket at round 5 (cost_array[8][NS] dominates)
+SCRATCH_MAX = {9: 384, 16: 672, 20: 816, 32: 1264}
 LDS_MAX = 160 * 1024 // 2  # two 256-thread blocks per CU (2 waves/SIMD)
 
 
