@@ -113,6 +113,10 @@ def collect(bench_py: str, child_args: list, out_dir: str, timeout: float = 150.
             return {"error": f"counter pass {name} exited {rc} (log {out_dir}/{name}.log)"}
         res["passes"][name] = {"counters": _counters(d), "durations_ms": _durations(d),
                                "wall_s": round(time.time() - t0, 1)}
+        # the per-dispatch CSVs are read: drop them (tens of MB per pass; the
+        # summary and the pass logs stay), so gpurun_out stays small enough
+        # to come back from the box
+        shutil.rmtree(d, ignore_errors=True)
     return summarize(res)
 
 
