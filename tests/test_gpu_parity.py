@@ -210,7 +210,9 @@ def test_t3_textureless(level, nan_share):
     - level 100: residual < 1e-5 -> every NCC 2, all sampling probabilities 0,
       weight norm 0 -> NaN costs (src/ACMMP.cu:1034, :1075, :1091);
     - level 77: residual > 1e-5 and var_ref == var_src == covar -> cost 0
-      everywhere except where the window leaves the source image.
+      wherever the centre maps into the source image, 2 (cost_max) for a view
+      where it does not (a border pixel's weighted mean can then be above 0),
+      NaN where no view was sampled.
     Both sides must agree bit-exactly either way."""
     W, H = 48, 40
     cams = []
@@ -226,7 +228,8 @@ def test_t3_textureless(level, nan_share):
     if nan_share is not None:
         assert nan.mean() == nan_share
     else:
-        assert 0 < nan.mean() < 0.1 and np.all(ref["costs"][~nan] == 0.0)
+        fin = ref["costs"][~nan]
+        assert 0 < nan.mean() < 0.1 and np.all((fin >= 0.0) & (fin <= 2.0)) and (fin == 0.0).mean() > 0.95
     assert_bit_exact(pl, ref["planes"], "planes")
     assert_bit_exact(co, ref["costs"], "costs")
 
