@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "acmmp_ctx.h"
+#include "../../include/acmmp_detmath.h"
 
 
 thread_local bool acmmp::g_frees_synced = false;
@@ -324,6 +325,18 @@ int kv_upload(acmmp_ctx *ctx) {
     if (const char *e = std::getenv("ACMMP_WIDE_INDEX"))
         if (e[0] == '1') kv.wide = 1;
     kv.texel = ctx->pad_texel;
+    if (kv.texel == kTexelU8) {  // bilateral weights of the 256 colour differences (KViews::wlut)
+        const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
+        for (int a = 0; a < 3; ++a)
+            for (int b = a; b < 3; ++b) {
+                const float xd = (float)(2 * a + 1), yd = (float)(2 * b + 1);
+                const float spatial = dm_sqrt(xd * xd + yd * yd);
+                for (int d = 0; d < 256; ++d) {
+                    const float color = (float)d;
+                    kv.wlut[wlut_class(a, b)][d] = dm_expf(-spatial / (2.0f * ss * ss) - color / (2.0f * sc * sc));
+                }
+            }
+    }
     kv.inv_k0 = 1.0f / ctx->cams[0].K[0];
     kv.inv_k4 = 1.0f / ctx->cams[0].K[4];
     kv.pert_pi = (float)((double)0.02f * M_PI);            // src/ACMMP.cu:737

@@ -66,7 +66,20 @@ struct KViews {
     int texel;                                // form of pad[]: kTexelF32 / kTexelU8 / kTexelH16
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
+    // Bilateral weights of ComputeBilateralWeight (src/ACMMP.cu:353-358) for
+    // an 8-bit reference image (texel == kTexelU8: every texel an integer in
+    // [0, 255], so |I - I_c| is one of 256 values): wlut[cls][d] =
+    // expf(-spatial_cls / (2 ss^2) - d / (2 sc^2)), cls = the tap's distance
+    // class (|dx|, |dy|) in {1, 3, 5}^2 up to order (kWlutClasses), formed on
+    // the host by the kernel's own float expression (same operations, same
+    // order: bit-identical to computing it per tap).
+    float wlut[6][256];
 };
+constexpr int kWlutClasses = 6;
+// distance class of |dx|, |dy| in {1, 3, 5}: (a, b) = ((|dx| - 1) / 2, (|dy| - 1) / 2), unordered
+__host__ __device__ constexpr int wlut_class(int a, int b) {
+    return a > b ? wlut_class(b, a) : (a == 0 ? b : (a == 1 ? 2 + b : 5));
+}
 
 struct KState {
     float4 *plane[2];       // colour-split current (read) planes, [colour]

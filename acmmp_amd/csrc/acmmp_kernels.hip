@@ -49,6 +49,18 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
+// per-call exact shortcuts of ComputeBilateralNCC's three divisions (A/B: 0 = IEEE divisions)
+#ifndef ACMMP_NCC_SHORTCUTS
+#define ACMMP_NCC_SHORTCUTS 1
+#endif
+// bilateral weights from the u8-form table (KViews::wlut; A/B: 0 = computed per tap)
+#ifndef ACMMP_WEIGHT_LUT
+#define ACMMP_WEIGHT_LUT 1
+#endif
+// the view selection's exact exp / division shortcuts (A/B: 0 = the literal forms)
+#ifndef ACMMP_VS_SHORTCUTS
+#define ACMMP_VS_SHORTCUTS 1
+#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -204,6 +216,36 @@ DEV float4 perturbed_normal(const acmmp_camera &c, int px, int py, float4 normal
     return np;
 }
 
+// Exactly rounded 1/z. The IEEE division sequence (v_div_scale / v_rcp /
+// 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. Inside the
+// exponent window below the sample loop replaces it by v_rcp_f32 + one fma
+// Newton step, which acmmp_selftest_reciprocal() proves bit-identical for
+// EVERY float in that window on this hardware.
+DEV float recip_newton(float z) {
+    const float r = __builtin_amdgcn_rcpf(z);
+    const float e = dm_fma(-z, r, 1.0f);
+    return dm_fma(e, r, r);
+}
+DEV bool recip_fast_window(float z) {
+    const float az = dm_fabs(z);
+    return az >= 0x1p-125f && az < 0x1p125f;
+}
+DEV float recip_exact(float z) { return 1.0f / z; }
+
+// IEEE 1/z computed as the Newton reciprocal where that is proven identical
+// (recip_fast_window: every float of it, acmmp_selftest_reciprocal), and as the
+// IEEE division only for lanes outside it (zeros, infinities, NaN, the extreme
+// binades): the same value in every case, fewer instructions in the common one.
+DEV float recip_any(float z) {
+#if ACMMP_NCC_SHORTCUTS
+    float r = recip_newton(z);
+    if (!recip_fast_window(z)) r = 1.0f / z;
+    return r;
+#else
+    return 1.0f / z;
+#endif
+}
+
 // ------------------------------------------------------ homography + NCC
 // ComputeHomography (src/ACMMP.cu:262-322) with the camera-only terms
 // precomputed per view (ViewRel) and pin P4.
@@ -211,7 +253,7 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
     const ViewRel &r = kv.rel[v];
     const acmmp_camera &rc = kv.cam[0];
     const acmmp_camera &sc = kv.cam[v];
-    const float inv_w = 1.0f / h.w;
+    const float inv_w = recip_any(h.w);
     float G[9];
     G[0] = r.Rr[0] - (r.tr[0] * h.x) * inv_w;
     G[1] = r.Rr[1] - (r.tr[0] * h.y) * inv_w;
@@ -244,28 +286,12 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
     H[8] = sc.K[8] * t[8];
 }
 
-// Exactly rounded 1/z. The IEEE division sequence (v_div_scale / v_rcp /
-// 4 fma / v_div_fmas / v_div_fixup) is the pinned semantics. Inside the
-// exponent window below the sample loop replaces it by v_rcp_f32 + one fma
-// Newton step, which acmmp_selftest_reciprocal() proves bit-identical for
-// EVERY float in that window on this hardware.
-DEV float recip_newton(float z) {
-    const float r = __builtin_amdgcn_rcpf(z);
-    const float e = dm_fma(-z, r, 1.0f);
-    return dm_fma(e, r, r);
-}
-DEV bool recip_fast_window(float z) {
-    const float az = dm_fabs(z);
-    return az >= 0x1p-125f && az < 0x1p125f;
-}
-DEV float recip_exact(float z) { return 1.0f / z; }
-
 // ComputeCorrespondingPoint (src/ACMMP.cu:324-331), pin P1
 DEV float2 project(const float *H, float x, float y) {
     const float px = dm_fma(H[1], y, dm_fma(H[0], x, H[2]));
     const float py = dm_fma(H[4], y, dm_fma(H[3], x, H[5]));
     const float pz = dm_fma(H[7], y, dm_fma(H[6], x, H[8]));
-    const float inv = recip_exact(pz);
+    const float inv = recip_any(pz);
     return make_float2(px * inv, py * inv);
 }
 
@@ -403,8 +429,17 @@ DEV float bilateral_weight(float xd, float yd, float pix, float cpix, float ss, 
     return dm_expf(-spatial / (2.0f * ss * ss) - color / (2.0f * sc * sc));
 }
 
-// tb = tile index of sample (ii=0, jj=0) of this lane: ty*kTileW + tx + s
-DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatch &pp) {
+// The bilateral-weight table (KViews::wlut) staged in LDS by the block
+// (kernels of the u8 texel form, whose reference texels are all integers in
+// [0, 255]); the caller's __syncthreads publishes it.
+DEV void load_wlut(const KViews &kv, float *wl) {
+    const int t = threadIdx.y * kBX + threadIdx.x;
+    for (int i = t; i < kWlutClasses * 256; i += kBX * kBY) wl[i] = (&kv.wlut[0][0])[i];
+}
+
+// tb = tile index of sample (ii=0, jj=0) of this lane: ty*kTileW + tx + s.
+// wlut: the LDS weight table (u8 texel form) or nullptr (weights computed).
+DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatch &pp, const float *wlut = nullptr) {
     const float ss = kv.prm.sigma_spatial, sc = kv.prm.sigma_color;
     const float center = tile[tb - s + 5 * kTileW + 3];
     float sum_ref = 0.0f, sum_rr = 0.0f, bw = 0.0f;
@@ -414,7 +449,12 @@ DEV void pixel_patch(const KViews &kv, const float *tile, int tb, int s, PixPatc
 #pragma unroll
         for (int jj = 0; jj < kTaps; ++jj) {
             const float r = tile[tb + ii + 2 * kTileW * jj];
-            const float w = bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
+            // |I - I_c| of integer texels in [0, 255]: the table holds the
+            // weight this expression gives for it (bit-identical)
+            const float w = wlut ? wlut[wlut_class((ii < 3 ? 5 - 2 * ii : 2 * ii - 5) / 2,
+                                                   (jj < 3 ? 5 - 2 * jj : 2 * jj - 5) / 2) * 256 +
+                                        (int)dm_fabs(r - center)]
+                                 : bilateral_weight((float)(-5 + 2 * ii), (float)(-5 + 2 * jj), r, center, ss, sc);
             const float wr = w * r;
             r_ref = dm_fma(w, r, r_ref);  // nvcc's contraction of `sum += w * r` (pin P3)
             r_rr = dm_fma(wr, r, r_rr);
@@ -702,7 +742,25 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     if (var_src < kMinVar) return cost_max;
     const float covar = dm_fma(sum_rs, pp.inv_wsum, -(pp.mean * sum_src));
     const float var_rs = dm_sqrt(pp.var * var_src);
-    float c = 1.0f - covar / var_rs;
+    // covar / var_rs: with y = 1 / var_rs exactly rounded (the Newton
+    // reciprocal in its proven window), q0 = covar * y, one exact fma residual
+    // and one fma correction give the IEEE quotient (Markstein), wherever the
+    // residual does not underflow; below that |q| < 2^-25 and 1 - q is the
+    // same either way. (1.6e9 random pairs, tools note in DESIGN §5: no
+    // difference.) Outside the reciprocal window: the IEEE division.
+    float q;
+#if ACMMP_NCC_SHORTCUTS
+    if (recip_fast_window(var_rs)) {
+        const float y = recip_newton(var_rs);
+        const float q0 = covar * y;
+        q = dm_fma(dm_fma(-var_rs, q0, covar), y, q0);
+    } else {
+        q = covar / var_rs;
+    }
+#else
+    q = covar / var_rs;
+#endif
+    float c = 1.0f - q;
     c = (c < cost_max) ? c : cost_max;
     c = (c > 0.0f) ? c : 0.0f;
     return c;
@@ -847,6 +905,7 @@ DEV dm_rng make_rng(const KViews &kv, int center, uint32_t phase) {
     g.phase = phase;
     g.stream = kv.prm.rng_stream;
     g.draw = 0;
+    g.blk = dm_u32x4{0u, 0u, 0u, 0u};
     return g;
 }
 
@@ -975,10 +1034,13 @@ template <int NS, int TX>
 __global__ __launch_bounds__(ACMMP_BLOCK_THREADS) void k_init(const KViews *__restrict__ kvp, KState st) {
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
+    constexpr bool kLut = (TX & kTxU8) != 0 && ACMMP_WEIGHT_LUT;
+    __shared__ float wlut[kLut ? kWlutClasses * 256 : 1];
     const KViews &kv = *kvp;
     const int colour = blockIdx.z;
     const BlockXY blk = xcd_block(st.y0 / kBY);
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    if (kLut) load_wlut(kv, wlut);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
     const int px = g.px, py = g.py;
@@ -991,7 +1053,7 @@ __global__ __launch_bounds__(ACMMP_BLOCK_THREADS) void k_init(const KViews *__re
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
     pp.rt = tile + g.tb;
-    pixel_patch(kv, tile, g.tb, g.s, pp);
+    pixel_patch(kv, tile, g.tb, g.s, pp, kLut ? wlut : nullptr);
     float4 plane;
     float cost;
     uint32_t sel = 0;
@@ -1171,9 +1233,12 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     __shared__ float tile[kTileW * kTileH];
     __shared__ WSlot wlds[kSlots * kThreads];
     __shared__ float4 cand_lds[8 * kThreads];
+    constexpr bool kLut = (TX & kTxU8) != 0 && ACMMP_WEIGHT_LUT;
+    __shared__ float wlut[kLut ? kWlutClasses * 256 : 1];
     const KViews &kv = *kvp;
     const BlockXY blk = xcd_block(st.y0 / kBY);
     load_ref_tile(kv, tile, blk.bx * kBX, blk.by * kBY, colour);
+    if (kLut) load_wlut(kv, wlut);
     __syncthreads();
     const LaneGeom g = lane_geom(colour, blk);
     const int px = g.px, py = g.py;
@@ -1302,7 +1367,7 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
     pp.wo = threadIdx.y * kBX + threadIdx.x;
     pp.w = wlds + pp.wo;
     pp.rt = tile + g.tb;
-    pixel_patch(kv, tile, g.tb, g.s, pp);
+    pixel_patch(kv, tile, g.tb, g.s, pp, kLut ? wlut : nullptr);
 
     // cost_array[8][32] = {2.0f}: only [0][0] is 2, the rest 0 (:805)
     float cost_array[8][NS];
@@ -1335,7 +1400,15 @@ DEV void sweep_body(const KViews *__restrict__ kvp, KState st, int colour, int i
             else c = (d == 0 && v == 0) ? 2.0f : 0.0f;
             cost_array[d][v] = c;
             if (c < cost_threshold) {
+                // exp(c * c / -0.18f) (:1017): c is 0 or in [2^-24, 2] (an NCC is 1 - q rounded,
+                // clamped to [0, 2]), so c * c is 0 or in [2^-48, 4] and the quotient in
+                // [-22.3, 0], where the Markstein quotient and dm_expf_nonpos are the IEEE
+                // quotient and dm_expf bit for bit (exhaustive: tests/test_detmath.py)
+#if ACMMP_VS_SHORTCUTS
+                tmpw += dm_expf_nonpos(dm_div_neg018(c * c));
+#else
                 tmpw += dm_expf(c * c / (-0.18f));
+#endif
                 count++;
             }
             if (c > 1.2f) count_false++;

@@ -78,6 +78,44 @@ DM_FN float dm_expf(float x) {
     return (er * dm_pow2i(k1)) * dm_pow2i(k2);
 }
 
+/* dm_expf on x in [-87, 0], for arguments known to lie there (the view
+ * selection's exp(-c^2 / 0.18), c in [0, 2]): dm_expf's common path without
+ * its NaN / overflow / underflow branches, and the scaling by 2^k (k in
+ * [-126, 0]) in one step, which is exact there as the two-step product is.
+ * Bit-identical to dm_expf for every float in [-87, 0]: checked exhaustively
+ * (tests/test_detmath.py::test_expf_nonpos_matches_expf). */
+DM_FN float dm_expf_nonpos(float x) {
+    const float kLog2e = 1.44269502162933349609375f;
+    const float kLn2Hi = 0.693145751953125f;
+    const float kLn2Lo = 1.428606765330187045e-06f;
+    const float kShift = 12582912.0f;
+    float t = x * kLog2e;
+    float kf = (t + kShift) - kShift;
+    float r = dm_fma(-kf, kLn2Hi, x);
+    r = dm_fma(-kf, kLn2Lo, r);
+    float p = 1.9875691500e-4f;
+    p = dm_fma(p, r, 1.3981999507e-3f);
+    p = dm_fma(p, r, 8.3334519073e-3f);
+    p = dm_fma(p, r, 4.1665795894e-2f);
+    p = dm_fma(p, r, 1.6666665459e-1f);
+    p = dm_fma(p, r, 5.0000001201e-1f);
+    float r2 = r * r;
+    float er = dm_fma(p, r2, r) + 1.0f;
+    return er * dm_pow2i((int)kf);
+}
+
+/* x / -0.18f for x in [0, 4] (the squared NCC costs of the view selection,
+ * src/ACMMP.cu:1017): q = x * RN(1 / -0.18), one fma residual, one fma
+ * correction (Markstein). Equal to the IEEE quotient for every float in
+ * [0, 4]: checked exhaustively (tests/test_detmath.py::
+ * test_div_by_neg018_matches_ieee). */
+DM_FN float dm_div_neg018(float x) {
+    const float r = 1.0f / -0.18f;  /* constant-folded, correctly rounded */
+    const float q = x * r;
+    const float e = dm_fma(0.18f, q, x);  /* x - (-0.18) q, exact */
+    return dm_fma(e, r, q);
+}
+
 /* sinf/cosf: Cephes single-precision reduction by pi/4 (3-part constant) and
  * the Cephes minimax polynomials. Valid for |x| < 8192 (PatchMatch only uses
  * |x| < 0.1: perturbation angles, src/ACMMP.cu:202-211). */
@@ -154,14 +192,19 @@ DM_FN float dm_acosf(float x) {
  * Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11), replacing the
  * reference's per-pixel curand XORWOW seeded from clock64()
  * (src/ACMMP.cu:624). Stateless: draw d of pixel `pix` in phase `phase` of
- * run `stream` is philox(key=seed, ctr={pix, d, phase, stream}).x.
+ * run `stream` is word d mod 4 of philox(key=seed, ctr={pix, d div 4, phase,
+ * stream}), so one Philox block serves four consecutive draws (r06; before,
+ * one block per draw, word 0 only).
  * The uniform mapping is curand_uniform's (0,1]: x * 2^-32 + 2^-33.
  * ------------------------------------------------------------------------- */
 DM_FN uint32_t dm_mulhi32(uint32_t a, uint32_t b) {
     return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
 }
-DM_FN uint32_t dm_philox_x(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
-                           uint32_t c2, uint32_t c3) {
+/* the four output words of one Philox4x32-10 block */
+typedef struct dm_u32x4 {
+    uint32_t x, y, z, w;
+} dm_u32x4;
+DM_FN dm_u32x4 dm_philox4(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
     for (int r = 0; r < 10; ++r) {
@@ -172,24 +215,33 @@ DM_FN uint32_t dm_philox_x(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += W0; k1 += W1;
     }
-    return c0;
+    dm_u32x4 o;
+    o.x = c0; o.y = c1; o.z = c2; o.w = c3;
+    return o;
+}
+DM_FN uint32_t dm_philox_x(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
+                           uint32_t c2, uint32_t c3) {
+    return dm_philox4(k0, k1, c0, c1, c2, c3).x;
 }
 DM_FN float dm_uniform(uint32_t x) {
     const float kInv2Pow32 = 2.3283064365386963e-10f;
     return (float)x * kInv2Pow32 + (kInv2Pow32 / 2.0f);
 }
 
-/* Per-pixel generator handle. */
+/* Per-pixel generator handle: the counter fields and the current block. */
 typedef struct dm_rng {
     uint32_t k0, k1;      /* seed */
     uint32_t pix;         /* ref-image pixel index y*W+x */
     uint32_t phase;       /* 0 = RandomInitialization, 1+i = iteration i */
     uint32_t stream;      /* RunPatchMatch call index on the engine */
     uint32_t draw;        /* running draw counter within (pix, phase) */
+    dm_u32x4 blk;         /* block draw / 4 (valid from the draw that fills it) */
 } dm_rng;
 
 DM_FN float dm_rng_uniform(dm_rng *g) {
-    uint32_t x = dm_philox_x(g->k0, g->k1, g->pix, g->draw, g->phase, g->stream);
+    const uint32_t w = g->draw & 3u;
+    if (w == 0u) g->blk = dm_philox4(g->k0, g->k1, g->pix, g->draw >> 2, g->phase, g->stream);
+    const uint32_t x = w == 0u ? g->blk.x : w == 1u ? g->blk.y : w == 2u ? g->blk.z : g->blk.w;
     g->draw += 1u;
     return dm_uniform(x);
 }

@@ -636,6 +636,7 @@ static dm_rng make_rng(const orc_state *S, int center, uint32_t phase) {
     g.phase = phase;
     g.stream = S->prm->rng_stream;
     g.draw = 0;
+    g.blk.x = g.blk.y = g.blk.z = g.blk.w = 0u;
     return g;
 }
 
@@ -1321,9 +1322,20 @@ void acmmp_oracle_homography(const acmmp_camera *ref, const acmmp_camera *src, c
     ComputeHomography(ref, src, h, H9);
 }
 
+/* draw `draw` of (pix, phase, stream): word draw mod 4 of block draw div 4 */
 float acmmp_oracle_uniform(uint32_t seed_lo, uint32_t seed_hi, uint32_t pix, uint32_t draw,
                            uint32_t phase, uint32_t stream) {
-    return dm_uniform(dm_philox_x(seed_lo, seed_hi, pix, draw, phase, stream));
+    dm_rng g;
+    g.k0 = seed_lo;
+    g.k1 = seed_hi;
+    g.pix = pix;
+    g.phase = phase;
+    g.stream = stream;
+    g.draw = draw & ~3u;
+    g.blk.x = g.blk.y = g.blk.z = g.blk.w = 0u;
+    float u = 0.0f;
+    for (uint32_t d = draw & ~3u; d <= draw; ++d) u = dm_rng_uniform(&g);
+    return u;
 }
 
 float acmmp_oracle_expf(float x) { return dm_expf(x); }
@@ -1335,6 +1347,15 @@ int acmmp_oracle_checkerboard_rows(int H) { return checkerboard_rows(H); }
 
 uint32_t acmmp_oracle_philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     return dm_philox_x(k0, k1, c0, c1, c2, c3);
+}
+
+void acmmp_oracle_philox4(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                          uint32_t *out4) {
+    const dm_u32x4 o = dm_philox4(k0, k1, c0, c1, c2, c3);
+    out4[0] = o.x;
+    out4[1] = o.y;
+    out4[2] = o.z;
+    out4[3] = o.w;
 }
 
 /* JBU_cu (src/ACMMP.cu:1458-1516) with RunJBU's Imagescale

@@ -54,6 +54,8 @@ def _load():
     lib.acmmp_oracle_homography.argtypes = [CAM, CAM, FP, FP]
     lib.acmmp_oracle_philox.restype = C.c_uint32
     lib.acmmp_oracle_philox.argtypes = [C.c_uint32] * 6
+    lib.acmmp_oracle_philox4.restype = None
+    lib.acmmp_oracle_philox4.argtypes = [C.c_uint32] * 6 + [U32P]
     lib.acmmp_oracle_uniform.restype = C.c_float
     lib.acmmp_oracle_uniform.argtypes = [C.c_uint32] * 6
     for name in ("expf", "sinf", "cosf", "acosf"):
@@ -205,6 +207,12 @@ def uniform(seed_lo, seed_hi, pix, draw, phase, stream):
 
 def philox_x(k0, k1, c0, c1, c2, c3):
     return int(_load().acmmp_oracle_philox(k0, k1, c0, c1, c2, c3))
+
+
+def philox4(k0, k1, c0, c1, c2, c3):
+    out = np.zeros(4, np.uint32)
+    _load().acmmp_oracle_philox4(k0, k1, c0, c1, c2, c3, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return [int(v) for v in out]
 
 
 def math_fn(name, x):
