@@ -49,10 +49,6 @@ constexpr int kWaveRows = ACMMP_WAVE_ROWS;  // rows of pixels per wave (lane_geo
 #define ACMMP_GEOM_AHEAD 7
 #endif
 constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
-// per-call exact shortcuts of ComputeBilateralNCC's three divisions (A/B: 0 = IEEE divisions)
-#ifndef ACMMP_NCC_SHORTCUTS
-#define ACMMP_NCC_SHORTCUTS 1
-#endif
 // bilateral weights from the u8-form table (KViews::wlut; A/B: 0 = computed per tap)
 #ifndef ACMMP_WEIGHT_LUT
 #define ACMMP_WEIGHT_LUT 1
@@ -232,19 +228,6 @@ DEV bool recip_fast_window(float z) {
 }
 DEV float recip_exact(float z) { return 1.0f / z; }
 
-// IEEE 1/z computed as the Newton reciprocal where that is proven identical
-// (recip_fast_window: every float of it, acmmp_selftest_reciprocal), and as the
-// IEEE division only for lanes outside it (zeros, infinities, NaN, the extreme
-// binades): the same value in every case, fewer instructions in the common one.
-DEV float recip_any(float z) {
-#if ACMMP_NCC_SHORTCUTS
-    float r = recip_newton(z);
-    if (!recip_fast_window(z)) r = 1.0f / z;
-    return r;
-#else
-    return 1.0f / z;
-#endif
-}
 
 // ------------------------------------------------------ homography + NCC
 // ComputeHomography (src/ACMMP.cu:262-322) with the camera-only terms
@@ -253,7 +236,7 @@ DEV void homography(const KViews &kv, int v, float4 h, float *H) {
     const ViewRel &r = kv.rel[v];
     const acmmp_camera &rc = kv.cam[0];
     const acmmp_camera &sc = kv.cam[v];
-    const float inv_w = recip_any(h.w);
+    const float inv_w = 1.0f / h.w;
     float G[9];
     G[0] = r.Rr[0] - (r.tr[0] * h.x) * inv_w;
     G[1] = r.Rr[1] - (r.tr[0] * h.y) * inv_w;
@@ -291,7 +274,7 @@ DEV float2 project(const float *H, float x, float y) {
     const float px = dm_fma(H[1], y, dm_fma(H[0], x, H[2]));
     const float py = dm_fma(H[4], y, dm_fma(H[3], x, H[5]));
     const float pz = dm_fma(H[7], y, dm_fma(H[6], x, H[8]));
-    const float inv = recip_any(pz);
+    const float inv = recip_exact(pz);
     return make_float2(px * inv, py * inv);
 }
 
@@ -742,25 +725,7 @@ DEV float bilateral_ncc(const KViews &kv, const float *tile, int tb, const PixPa
     if (var_src < kMinVar) return cost_max;
     const float covar = dm_fma(sum_rs, pp.inv_wsum, -(pp.mean * sum_src));
     const float var_rs = dm_sqrt(pp.var * var_src);
-    // covar / var_rs: with y = 1 / var_rs exactly rounded (the Newton
-    // reciprocal in its proven window), q0 = covar * y, one exact fma residual
-    // and one fma correction give the IEEE quotient (Markstein), wherever the
-    // residual does not underflow; below that |q| < 2^-25 and 1 - q is the
-    // same either way. (1.6e9 random pairs, tools note in DESIGN §5: no
-    // difference.) Outside the reciprocal window: the IEEE division.
-    float q;
-#if ACMMP_NCC_SHORTCUTS
-    if (recip_fast_window(var_rs)) {
-        const float y = recip_newton(var_rs);
-        const float q0 = covar * y;
-        q = dm_fma(dm_fma(-var_rs, q0, covar), y, q0);
-    } else {
-        q = covar / var_rs;
-    }
-#else
-    q = covar / var_rs;
-#endif
-    float c = 1.0f - q;
+    float c = 1.0f - covar / var_rs;
     c = (c < cost_max) ? c : cost_max;
     c = (c > 0.0f) ? c : 0.0f;
     return c;

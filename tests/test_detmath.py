@@ -118,7 +118,7 @@ int main(void) {
         if (dm_f2u(dm_expf(x)) != dm_f2u(dm_expf_nonpos(x))) bad_exp++;
     }
     if (dm_f2u(dm_expf(0.0f)) != dm_f2u(dm_expf_nonpos(0.0f))) bad_exp++;
-    /* k_sweep's NCC quotient covar / var_rs as a Markstein quotient on the
+    /* (the round-6 A/B variant of DESIGN §5, not the product) the NCC quotient covar / var_rs as a Markstein quotient on the
      * exactly rounded reciprocal (the device's Newton reciprocal equals IEEE
      * 1/z in its window, acmmp_selftest_reciprocal): 1.6e9 random pairs,
      * var_rs normal in [2^-20, 2^20], covar 0 or of either sign in
