@@ -60,6 +60,12 @@ struct acmmp_ctx {
     int cur[2] = {0, 0};
     float4 *d_rm_plane = nullptr;
     float *d_rm_cost = nullptr;
+    // depth channel of d_rm_plane as its own plane (written by k_finalize and
+    // the filters: the filters read 4 B per neighbour instead of a float4, and
+    // the depth export is a plain copy); depth_ok: it matches d_rm_plane's .w
+    // (set by a full run, cleared by every other writer of d_rm_plane)
+    float *d_rm_depth = nullptr;
+    bool depth_ok = false;
     uint32_t *d_rm_sv = nullptr;
     float *d_pre_cost = nullptr;
     float4 *d_prior = nullptr;

@@ -247,6 +247,8 @@ void free_state(acmmp_ctx *ctx) {
     }
     dfree(ctx->d_rm_plane);
     dfree(ctx->d_rm_cost);
+    dfree(ctx->d_rm_depth);
+    ctx->depth_ok = false;
     dfree(ctx->d_rm_sv);
     dfree(ctx->d_pre_cost);
     dfree(ctx->d_prior);
@@ -373,6 +375,7 @@ KState state_of(acmmp_ctx *ctx, int y0 = 0, int y1 = -1) {
     }
     st.rm_plane = ctx->d_rm_plane;
     st.rm_cost = ctx->d_rm_cost;
+    st.rm_depth = ctx->d_rm_depth;
     st.rm_sv = ctx->d_rm_sv;
     st.pre_cost = ctx->d_pre_cost;
     st.prior = ctx->d_prior;
@@ -578,12 +581,14 @@ int set_images_impl(acmmp_ctx *ctx, int num_images, const acmmp_camera *cams, co
         }
         HIP_TRY(ctx, dalloc(ctx->d_rm_plane, P));
         HIP_TRY(ctx, dalloc(ctx->d_rm_cost, P));
+        HIP_TRY(ctx, dalloc(ctx->d_rm_depth, P));
         HIP_TRY(ctx, dalloc(ctx->d_rm_sv, P));
         HIP_TRY(ctx, dalloc(ctx->d_pre_cost, P));
         // zero-filled state (pin: the reference's never-written host fields,
         // src/ACMMP.cpp:797-804, and uninitialised pre_costs)
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_plane, 0, P * sizeof(float4), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_cost, 0, P * sizeof(float), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_depth, 0, P * sizeof(float), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_rm_sv, 0, P * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_pre_cost, 0, P * sizeof(float), ctx->stream));
         for (int c = 0; c < 2; ++c) HIP_TRY(ctx, hipMemsetAsync(ctx->d_csv[c], 0, Pc * sizeof(uint32_t), ctx->stream));
@@ -903,6 +908,7 @@ int acmmp_set_plane_hypotheses(acmmp_ctx *ctx, const float *planes4, const float
     if (rc) return rc;
     if (!planes4 || !costs) return set_err(ctx, ACMMP_ERR_ARG, "planes/costs NULL");
     const size_t P = (size_t)ctx->W * ctx->H;
+    ctx->depth_ok = false;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, planes4, P * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_cost, costs, P * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -915,6 +921,7 @@ int acmmp_set_plane_hypotheses_device(acmmp_ctx *ctx, const float *d_planes4, co
     if (rc) return rc;
     if (!d_planes4 || !d_costs) return set_err(ctx, ACMMP_ERR_ARG, "planes/costs NULL");
     const size_t P = (size_t)ctx->W * ctx->H;
+    ctx->depth_ok = false;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, d_planes4, P * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_cost, d_costs, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     ctx->have_state = true;
@@ -940,7 +947,9 @@ int acmmp_export_results(acmmp_ctx *ctx, float *d_planes4, float *d_costs, float
         HIP_TRY(ctx, hipMemcpyAsync(d_planes4, ctx->d_rm_plane, P * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
     if (d_costs)
         HIP_TRY(ctx, hipMemcpyAsync(d_costs, ctx->d_rm_cost, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
-    if (d_depth)  // the .w channel: strided 2-D copy, 4 B out of every 16 B
+    if (d_depth && ctx->depth_ok)  // the depth plane the last full run wrote: a plain copy
+        HIP_TRY(ctx, hipMemcpyAsync(d_depth, ctx->d_rm_depth, P * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    else if (d_depth)  // the .w channel: strided 2-D copy, 4 B out of every 16 B
         HIP_TRY(ctx, hipMemcpy2DAsync(d_depth, sizeof(float), (const char *)ctx->d_rm_plane + 3 * sizeof(float),
                                       sizeof(float4), sizeof(float), P, hipMemcpyDeviceToDevice, ctx->stream));
     return ACMMP_OK;
@@ -963,10 +972,12 @@ int set_hierarchy_impl(acmmp_ctx *ctx, const float *scaled_planes4, int scaled_w
     // plane_hypotheses_host[center].w = ref_depth; x, y, z never written (pinned 0)
     const size_t P = (size_t)ctx->W * ctx->H;
     if (device_src) {
+        ctx->depth_ok = false;
         HIP_TRY(ctx, launch_depth_planes(upsampled_depth, P, ctx->d_rm_plane, ctx->stream));
     } else {
         std::vector<float> tmp(P * 4, 0.0f);
         for (size_t i = 0; i < P; ++i) tmp[i * 4 + 3] = upsampled_depth[i];
+        ctx->depth_ok = false;
         HIP_TRY(ctx, hipMemcpyAsync(ctx->d_rm_plane, tmp.data(), P * sizeof(float4), hipMemcpyHostToDevice,
                                     ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // tmp goes out of scope
@@ -1082,6 +1093,7 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
     HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 0, s));
     HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx), 1, s));
+    ctx->depth_ok = true;  // every pixel's depth: finalize + filters over the whole image
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[3], s));
     ctx->prm.rng_stream += 1u;  // a further RunPatchMatch re-seeds (clock64() in the reference)
     ctx->have_state = true;
@@ -1133,6 +1145,7 @@ int acmmp_run_patchmatch_band(acmmp_ctx *ctx, int row_lo, int row_hi, acmmp_band
     // CheckerboardFilter reads +-5 rows (src/ACMMP.cu:1214-1328): depth /
     // normal conversion on the band +-10 rows (valid halos), the black filter
     // on the band +-5 rows (what the red filter reads), the red one on the band
+    ctx->depth_ok = false;  // rows outside the band keep older depths
     HIP_TRY(ctx, launch_finalize(ctx->d_kv, ctx->h_kv, state_of(ctx, std::max(0, row_lo - 10), std::min(H, row_hi + 10)), s));
     HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx, std::max(0, row_lo - 5), std::min(H, row_hi + 5)), 0, s));
     HIP_TRY(ctx, launch_filter(ctx->d_kv, ctx->h_kv, state_of(ctx, row_lo, row_hi), 1, s));

@@ -89,6 +89,7 @@ struct KState {
     uint32_t *sv[2];        // colour-split selected views (in place)
     float4 *rm_plane;       // row-major state between runs
     float *rm_cost;
+    float *rm_depth;        // rm_plane[.].w as its own plane (finalize and filters)
     uint32_t *rm_sv;
     float *pre_cost;        // hierarchy (row-major)
     const float4 *prior;    // planar prior planes (row-major)

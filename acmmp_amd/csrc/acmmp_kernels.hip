@@ -1755,6 +1755,7 @@ __global__ __launch_bounds__(256) void k_finalize(const KViews *__restrict__ kvp
     h = to_world(kv.cam[0], h);
     const int center = py * kv.W + px;
     st.rm_plane[center] = h;
+    st.rm_depth[center] = h.w;
     st.rm_cost[center] = st.cost[c][ci];
     st.rm_sv[center] = st.sv[c][ci];
 }
@@ -1769,36 +1770,38 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
     if (py < st.y0 || py >= st.y1 || py >= kv.sweep_rows) return;
     const int px = 2 * k + ((py + colour) & 1);
     if (px >= width) return;
-    float4 *ph = st.rm_plane;
+    // neighbours' depths from the depth plane (4 B each; the same values as
+    // rm_plane[.].w, which the filter updates alongside)
+    const float *ph = st.rm_depth;
     const int center = py * width + px;
     if (st.rm_cost[center] < 0.001f) return;
     float f[21];
     int n = 0;
-    f[n++] = ph[center].w;
+    f[n++] = ph[center];
     const int left = center - 1, leftleft = center - 3;
     const int up = center - width, upup = center - 3 * width;
     const int down = center + width, downdown = center + 3 * width;
     const int right = center + 1, rightright = center + 3;
-    if (py > 0) f[n++] = ph[up].w;
-    if (py > 2) f[n++] = ph[upup].w;
-    if (py > 4) f[n++] = ph[upup - width * 2].w;
-    if (py < height - 1) f[n++] = ph[down].w;
-    if (py < height - 3) f[n++] = ph[downdown].w;
-    if (py < height - 5) f[n++] = ph[downdown + width * 2].w;
-    if (px > 0) f[n++] = ph[left].w;
-    if (px > 2) f[n++] = ph[leftleft].w;
-    if (px > 4) f[n++] = ph[leftleft - 2].w;
-    if (px < width - 1) f[n++] = ph[right].w;
-    if (px < width - 3) f[n++] = ph[rightright].w;
-    if (px < width - 5) f[n++] = ph[rightright + 2].w;
-    if (py > 0 && px < width - 2) f[n++] = ph[up + 2].w;
-    if (py < height - 1 && px < width - 2) f[n++] = ph[down + 2].w;
-    if (py > 0 && px > 1) f[n++] = ph[up - 2].w;
-    if (py < height - 1 && px > 1) f[n++] = ph[down - 2].w;
-    if (px > 0 && py > 2) f[n++] = ph[left - width * 2].w;
-    if (px < width - 1 && py > 2) f[n++] = ph[right - width * 2].w;
-    if (px > 0 && py < height - 2) f[n++] = ph[left + width * 2].w;
-    if (px < width - 1 && py < height - 2) f[n++] = ph[right + width * 2].w;
+    if (py > 0) f[n++] = ph[up];
+    if (py > 2) f[n++] = ph[upup];
+    if (py > 4) f[n++] = ph[upup - width * 2];
+    if (py < height - 1) f[n++] = ph[down];
+    if (py < height - 3) f[n++] = ph[downdown];
+    if (py < height - 5) f[n++] = ph[downdown + width * 2];
+    if (px > 0) f[n++] = ph[left];
+    if (px > 2) f[n++] = ph[leftleft];
+    if (px > 4) f[n++] = ph[leftleft - 2];
+    if (px < width - 1) f[n++] = ph[right];
+    if (px < width - 3) f[n++] = ph[rightright];
+    if (px < width - 5) f[n++] = ph[rightright + 2];
+    if (py > 0 && px < width - 2) f[n++] = ph[up + 2];
+    if (py < height - 1 && px < width - 2) f[n++] = ph[down + 2];
+    if (py > 0 && px > 1) f[n++] = ph[up - 2];
+    if (py < height - 1 && px > 1) f[n++] = ph[down - 2];
+    if (px > 0 && py > 2) f[n++] = ph[left - width * 2];
+    if (px < width - 1 && py > 2) f[n++] = ph[right - width * 2];
+    if (px > 0 && py < height - 2) f[n++] = ph[left + width * 2];
+    if (px < width - 1 && py < height - 2) f[n++] = ph[right + width * 2];
     for (int i = 1; i < n; i++) {  // sort_small
         const float tmp = f[i];
         int j;
@@ -1806,7 +1809,9 @@ __global__ __launch_bounds__(256) void k_filter(const KViews *__restrict__ kvp, 
         f[j] = tmp;
     }
     const int m = n / 2;
-    ph[center].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
+    const float med = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
+    st.rm_depth[center] = med;
+    st.rm_plane[center].w = med;
 }
 
 __global__ __launch_bounds__(256) void k_eval_geom(const KViews *__restrict__ kvp, const float4 *planes,
