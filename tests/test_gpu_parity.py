@@ -96,6 +96,39 @@ def test_t1_geom_cost(small_scene):
     assert_bit_exact(g, r, "geometric consistency cost")
 
 
+def test_t1_geom_cost_extreme_values(small_scene):
+    """The geometric cost's quotients outside and on the edge of the Markstein
+    window (quot2 / quot_focal): source depths 0, +-inf, NaN, negative,
+    subnormal, tiny and huge, and hypotheses whose depth is 0, NaN, tiny or
+    huge, against the oracle's IEEE divisions."""
+    cams, imgs = small_scene.problem(0, 4)
+    ids = [0] + small_scene.pairs[0][:4]
+    H, W = imgs[0].shape
+    rng = np.random.default_rng(11)
+    special = np.array([0.0, np.inf, -np.inf, np.nan, -500.0, 1e-40, 1e-30, 2.0 ** -61, 2.0 ** -59,
+                        2.0 ** 59, 2.0 ** 61, 1e30, 3e38], np.float32)
+    depths = []
+    for i in ids:
+        d = small_scene.views[i].depth.astype(np.float32).copy()
+        m = rng.random(d.shape) < 0.3
+        d[m] = rng.choice(special, size=int(m.sum()))
+        depths.append(d)
+    planes = _random_planes(cams, H, W, seed=5)
+    scale = np.array([1.0, 0.0, np.nan, 1e-30, 2.0 ** -62, 2.0 ** 62, 1e30, -1.0], np.float32)
+    m = rng.random((H, W)) < 0.3
+    planes[..., 3][m] *= rng.choice(scale, size=int(m.sum()))
+    p = _params(geom_consistency=1)
+    with ACMMP(0) as eng:
+        eng.set_params(p)
+        eng.set_images(cams, imgs)
+        eng.set_depth_maps(depths)
+        prm = eng.params
+        g = eng.eval_geom_costs(planes)
+    r = oracle.eval_geom_costs(prm, cams, imgs, depths, planes)
+    assert_bit_exact(g, r, "geometric consistency cost, extreme values")
+    assert np.isfinite(r).mean() > 0.5 and (r < 3.0).mean() > 0.05
+
+
 @pytest.mark.parametrize("iters", [0, 1])
 def test_t2_init_and_one_sweep(small_scene, iters):
     cams, imgs = small_scene.problem(0, 9)
@@ -261,6 +294,20 @@ def test_fast_reciprocal_is_exact_on_this_device():
     m, n = C.c_uint64(), C.c_uint64()
     assert _abi.load_library().acmmp_selftest_reciprocal(0, C.byref(m), C.byref(n)) == 0
     assert n.value == 2 * 250 * (1 << 23)  # both signs, exponents -125..124, all mantissas
+    assert m.value == 0
+
+
+def test_geometric_quotients_are_exact_on_this_device():
+    """The geometric cost's quotients (quot2 / quot_focal: Markstein's
+    correction on RN(1/b) finished by v_div_fixup) must equal the IEEE
+    division for every pair of significands — with every intermediate normal
+    in the window |a|, |b| in [2^-60, 2^60) the results scale with the
+    exponents and signs, so the 2^46 pairs cover the whole window."""
+    import ctypes as C
+    from acmmp_amd import _abi
+    m, n = C.c_uint64(), C.c_uint64()
+    assert _abi.load_library().acmmp_selftest_quotient(0, C.byref(m), C.byref(n)) == 0
+    assert n.value == 1 << 46
     assert m.value == 0
 
 
