@@ -211,7 +211,6 @@ SIGNATURES = {
     "acmmp_set_timing": (C.c_int, [_CTX, C.c_int]),
     "acmmp_get_timing": (C.c_int, [_CTX, C.POINTER(Timing)]),
     "acmmp_selftest_reciprocal": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
-    "acmmp_selftest_quotient": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "acmmp_get_texel_bits": (C.c_int, [_CTX]),
     "acmmp_device_count": (C.c_int, []),
     "acmmp_version": (C.c_char_p, []),

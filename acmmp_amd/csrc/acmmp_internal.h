@@ -65,11 +65,6 @@ struct KViews {
     int wide;                                 // some view has >= 2^24 padded records
     int texel;                                // form of pad[]: kTexelF32 / kTexelU8 / kTexelH16
     float inv_k0, inv_k4;                     // 1/K[0], 1/K[4] of the ref camera (pin P4)
-    // RN(1/K[0]), RN(1/K[4]) of every camera (host IEEE division) for the
-    // geometric cost's exact Markstein quotients (quot_focal); quot_ok: every
-    // camera's two focal lengths lie in the quotient window [2^-60, 2^60)
-    float ifk[ACMMP_MAX_IMAGES][2];
-    int quot_ok;
     float pert_pi, pert3_pi, angle_sigma;     // double-precision constants of the reference
     // Bilateral weights of ComputeBilateralWeight (src/ACMMP.cu:353-358) for
     // an 8-bit reference image (texel == kTexelU8: every texel an integer in
@@ -132,7 +127,6 @@ hipError_t launch_depth_planes(const float *depth, size_t n, float4 *out, hipStr
 hipError_t launch_jbu(const float *img, int W, int H, const float *depth, int sw, int sh, int image_scale,
                       float *out, hipStream_t stream);
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s);
-hipError_t launch_selftest_quot(uint32_t b0, unsigned long long *mismatch, hipStream_t s);
 
 // Number of checkerboard rows the reference grid reaches (src/ACMMP.cu:1399).
 inline int checkerboard_rows(int H) {

@@ -57,15 +57,6 @@ constexpr int kSweepWaves = 2; // __launch_bounds__ waves per SIMD of k_sweep
 #ifndef ACMMP_VS_SHORTCUTS
 #define ACMMP_VS_SHORTCUTS 1
 #endif
-// the geometric cost's quotients as Markstein quotients inside their proven
-// window (quot2 below; A/B: 0 = the IEEE division sequence everywhere). Off
-// in the fidelity-study build, whose divisions follow nvcc's flags.
-#if !defined(ACMMP_GEOM_QUOT) && defined(ACMMP_CUDA_NUMERICS)
-#define ACMMP_GEOM_QUOT 0
-#endif
-#ifndef ACMMP_GEOM_QUOT
-#define ACMMP_GEOM_QUOT 1
-#endif
 
 // ----------------------------------------------------------------- textures
 // Through the global address space: a generic (flat) load would also count
@@ -236,29 +227,6 @@ DEV bool recip_fast_window(float z) {
     return az >= 0x1p-125f && az < 0x1p125f;
 }
 DEV float recip_exact(float z) { return 1.0f / z; }
-
-// Exactly rounded a / b from y = RN(1/b): Markstein's correction
-// (q0 = a y, r = fma(-q0, b, a), q = fma(r, y, q0); 4 VALU against the
-// division sequence's 10) finished by v_div_fixup, whose special-operand
-// rules (NaN, 0, inf in a or b) depend on a and b only, exactly as in the
-// IEEE sequence's own final fixup. In quot_window (|a|, |b| in
-// [2^-60, 2^60)) every intermediate is normal and no remainder underflows, so
-// the result scales with the exponents and depends on the two significands
-// only: acmmp_selftest_quotient() checks all 2^46 significand pairs against
-// the IEEE division on the device.
-DEV float quot_markstein(float a, float b, float y) {
-    const float q0 = a * y;
-    const float r = dm_fma(-q0, b, a);
-    return __builtin_amdgcn_div_fixupf(dm_fma(r, y, q0), b, a);
-}
-// lo / hi: the smallest / largest magnitude of the operands. A NaN operand
-// drops out of fminf / fmaxf; the fixup then returns the IEEE NaN anyway.
-DEV bool quot_window(float lo, float hi) {
-#ifdef ACMMP_UB_QUOT_ALWAYS  // timing-only bound: no window test, no branch (wrong outside the window)
-    return true;
-#endif
-    return lo >= 0x1p-60f && hi < 0x1p60f;
-}
 
 
 // ------------------------------------------------------ homography + NCC
@@ -821,47 +789,12 @@ DEV float cam_offset(const KViews &kv, int v, int k) {
 #endif
 }
 
-// nx / d and ny / d (one shared, per-lane denominator): IEEE-exact. Inside
-// the window the reciprocal is recip_newton (= RN(1/d) there, the
-// reciprocal self-test) and the quotients quot_markstein; any lane outside
-// it takes the division sequence.
-DEV void quot2(float nx, float ny, float d, float &qx, float &qy) {
-#if ACMMP_GEOM_QUOT
-    const float lo = fminf(fminf(fabsf(nx), fabsf(ny)), fabsf(d));
-    const float hi = fmaxf(fmaxf(fabsf(nx), fabsf(ny)), fabsf(d));
-    if (quot_window(lo, hi)) {
-        const float y = recip_newton(d);
-        qx = quot_markstein(nx, d, y);
-        qy = quot_markstein(ny, d, y);
-        return;
-    }
-#endif
-    qx = nx / d;
-    qy = ny / d;
-}
-
-// n0 / K[0] and n1 / K[4] of camera v: IEEE-exact. The reciprocals are the
-// host's RN(1/K) (KViews::ifk); KViews::quot_ok says both focal lengths of
-// every view lie in the window.
-DEV void quot_focal(const KViews &kv, int v, float n0, float n1, float &q0, float &q1) {
-    const acmmp_camera &c = kv.cam[v];
-#if ACMMP_GEOM_QUOT
-    if (kv.quot_ok && quot_window(fminf(fabsf(n0), fabsf(n1)), fmaxf(fabsf(n0), fabsf(n1)))) {
-        q0 = quot_markstein(n0, c.K[0], kv.ifk[v][0]);
-        q1 = quot_markstein(n1, c.K[4], kv.ifk[v][1]);
-        return;
-    }
-#endif
-    q0 = n0 / c.K[0];
-    q1 = n1 / c.K[4];
-}
-
 DEV GeomRef geom_ref(const KViews &kv, float4 h, int px, int py) {
     const acmmp_camera &rc = kv.cam[0];
     const float depth = plane_depth(rc, h, px, py);
     float X[3];
-    // depth * (px - K[2]) / K[0], depth * (py - K[5]) / K[4]
-    quot_focal(kv, 0, depth * ((float)px - rc.K[2]), depth * ((float)py - rc.K[5]), X[0], X[1]);
+    X[0] = depth * ((float)px - rc.K[2]) / rc.K[0];
+    X[1] = depth * ((float)py - rc.K[5]) / rc.K[4];
     X[2] = depth;
     GeomRef g;
     g.Wp[0] = (rc.R[0] * X[0] + rc.R[3] * X[1] + rc.R[6] * X[2]) + cam_offset(kv, 0, 0);
@@ -888,8 +821,8 @@ DEV GeomFetch geom_fetch(const KViews &kv, int v, const GeomRef &g) {
     T[2] = sc.R[6] * Wp[0] + sc.R[7] * Wp[1] + sc.R[8] * Wp[2] + sc.t[2];
     const float sd = sc.K[6] * T[0] + sc.K[7] * T[1] + sc.K[8] * T[2];
     GeomFetch f;
-    quot2(sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2], sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2], sd,
-          f.sx, f.sy);
+    f.sx = (sc.K[0] * T[0] + sc.K[1] * T[1] + sc.K[2] * T[2]) / sd;
+    f.sy = (sc.K[3] * T[0] + sc.K[4] * T[1] + sc.K[5] * T[2]) / sd;
     f.dep = tex_trunc(kv.dep[v], kv.dpitch[v], kv.dw[v], kv.dh[v], f.sx, f.sy);
     return f;
 }
@@ -901,8 +834,8 @@ DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int p
     const float sx = f.sx, sy = f.sy, src_depth = f.dep;
     if (src_depth == 0.0f) return max_cost;
     float Y[3];
-    // src_depth * (sx - K[2]) / K[0], src_depth * (sy - K[5]) / K[4]
-    quot_focal(kv, v, src_depth * (sx - sc.K[2]), src_depth * (sy - sc.K[5]), Y[0], Y[1]);
+    Y[0] = src_depth * (sx - sc.K[2]) / sc.K[0];
+    Y[1] = src_depth * (sy - sc.K[5]) / sc.K[4];
     Y[2] = src_depth;
     float Wq[3];
     Wq[0] = (sc.R[0] * Y[0] + sc.R[3] * Y[1] + sc.R[6] * Y[2]) + cam_offset(kv, v, 0);
@@ -913,9 +846,8 @@ DEV float geom_finish(const KViews &kv, int v, const GeomFetch &f, int px, int p
     U[1] = rc.R[3] * Wq[0] + rc.R[4] * Wq[1] + rc.R[5] * Wq[2] + rc.t[1];
     U[2] = rc.R[6] * Wq[0] + rc.R[7] * Wq[1] + rc.R[8] * Wq[2] + rc.t[2];
     const float rd = rc.K[6] * U[0] + rc.K[7] * U[1] + rc.K[8] * U[2];
-    float bx, by;
-    quot2(rc.K[0] * U[0] + rc.K[1] * U[1] + rc.K[2] * U[2], rc.K[3] * U[0] + rc.K[4] * U[1] + rc.K[5] * U[2], rd,
-          bx, by);
+    const float bx = (rc.K[0] * U[0] + rc.K[1] * U[1] + rc.K[2] * U[2]) / rd;
+    const float by = (rc.K[3] * U[0] + rc.K[4] * U[1] + rc.K[5] * U[2]) / rd;
     const float dc = (float)px - bx;
     const float dr = (float)py - by;
     const float e = dm_sqrt(dc * dc + dr * dr);
@@ -1996,31 +1928,6 @@ __global__ __launch_bounds__(256) void k_selftest_rcp(unsigned long long *mismat
 
 hipError_t launch_selftest_rcp(unsigned long long *mismatch, unsigned long long *checked, hipStream_t s) {
     k_selftest_rcp<<<4096, 256, 0, s>>>(mismatch, checked);
-    return hipGetLastError();
-}
-
-// Exhaustive check of quot_markstein (with y = recip_newton(b), as quot2
-// forms it; equal to the host's RN(1/b) by the reciprocal self-test) against
-// the IEEE division a / b for every pair of significands a, b in [1, 2)
-// (2^46 pairs; in quot_window the results scale with the exponents and the
-// signs). One launch: significands b = b0 .. b0 + 2^14 - 1, each against
-// all 2^23 a; thread t takes b0 + (t >> 9) and a = ((t & 511) << 14) + i.
-constexpr int kQuotBPerLaunch = 1 << 14;
-__global__ __launch_bounds__(256) void k_selftest_quot(uint32_t b0, unsigned long long *mismatch) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const float b = __uint_as_float(0x3f800000u | (b0 + (t >> 9)));
-    const float y = recip_newton(b);
-    const uint32_t a0 = (t & 511u) << 14;
-    unsigned long long bad = 0;
-    for (uint32_t i = 0; i < (1u << 14); ++i) {
-        const float a = __uint_as_float(0x3f800000u | (a0 + i));
-        if (__float_as_uint(quot_markstein(a, b, y)) != __float_as_uint(a / b)) ++bad;
-    }
-    if (bad) atomicAdd(mismatch, bad);
-}
-
-hipError_t launch_selftest_quot(uint32_t b0, unsigned long long *mismatch, hipStream_t s) {
-    k_selftest_quot<<<(kQuotBPerLaunch << 9) / 256, 256, 0, s>>>(b0, mismatch);
     return hipGetLastError();
 }
 

@@ -383,15 +383,6 @@ int acmmp_get_timing(const acmmp_ctx *ctx, acmmp_timing *t);
  * bit-identical to the pinned division on this device. */
 int acmmp_selftest_reciprocal(int device, uint64_t *mismatches, uint64_t *checked);
 
-/* Hardware self-test of the geometric cost's exact quotients: the Markstein
- * sequence (q0 = a y, r = fma(-q0, b, a), fma(r, y, q0), v_div_fixup) with
- * y = v_rcp_f32 + one Newton step, against the IEEE division a / b for every
- * pair of significands a, b in [1, 2) (checked = 2^46; about half a minute).
- * mismatches == 0 proves the quotients bit-identical to the pinned division
- * for all |a|, |b| in [2^-60, 2^60) on this device (the results scale with
- * the exponents there). No reference counterpart (diagnostic). */
-int acmmp_selftest_quotient(int device, uint64_t *mismatches, uint64_t *checked);
-
 /* Texel storage the gather kernels use for the current images (set by
  * acmmp_set_images*): 8 = u8 quads (the default whenever every view is
  * integer-valued in [0, 255], e.g. 8-bit JPEG input), 16 = f16 difference
