@@ -1079,6 +1079,7 @@ int acmmp_run_patchmatch_async(acmmp_ctx *ctx) {
     if (rc) return rc;
     const acmmp_params &p = ctx->prm;
     hipStream_t s = ctx->stream;
+    ctx->depth_ok = false;  // until this run's filters are queued (a failed run leaves the strided export)
     if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->ev[0], s));
     ctx->cur[0] = ctx->cur[1] = 0;
     HIP_TRY(ctx, launch_init(ctx->d_kv, ctx->h_kv, state_of(ctx), s));
